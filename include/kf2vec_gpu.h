@@ -1,0 +1,139 @@
+/*
+ * kf2vec_gpu.h -- C-ABI of the MI355X (gfx950) k-mer frequency-vector builder.
+ *
+ * Drop-in boundary for kf2vec's `get_frequencies` hot path
+ * (reference kf2vec/main.py:250-373).  The reference crosses a PROCESS boundary
+ * there: it runs the external C++ counter Jellyfish twice per genome
+ *     jellyfish count -m K -s 100M -t P -C <in> -o <x>.jf     (main.py:309-311)
+ *     jellyfish dump -c <x>.jf_0 > <x>.dump                    (main.py:317-319)
+ * then pandas-joins the dump onto the sorted canonical vocabulary
+ * (main.py:278-296, 323-328), normalises (332-342) and formats one `.kf` line
+ * (344-357).  This library replaces all of that with device kernels plus a
+ * host formatter; the Python host (kf2vecfsw_amd/) binds it with ctypes.
+ *
+ * Conventions
+ *   - plain pointers and sizes only; `d_` pointers are device (HBM) pointers,
+ *     e.g. `torch.Tensor.data_ptr()` of a ROCm tensor; the CALLER owns every buffer;
+ *   - `stream` is a hipStream_t (NULL = default stream); device entry points only
+ *     enqueue work (no host sync, no allocation) so they can be graph-captured;
+ *   - return 0 on success, a negative KF_E* code on failure; the message is in
+ *     kf_last_error() (thread-local).  Errors are never silent (deliberate
+ *     deviation from main.py:309-311, which discards Jellyfish's stderr/status).
+ *
+ * Internal 2-bit base code ("kf code"): A=0 C=1 T=2 G=3, i.e. ((ascii >> 1) & 3)
+ * for ACGTacgt; complement = code ^ 2.  A k-mer code has its first base in the
+ * most significant pair.  Columns (bins) are the rank of the canonical k-mer in
+ * the lexicographically sorted canonical vocabulary -- the order of the
+ * reference's vocab files (kf2vec/data/) and hence of every `.kf` line.
+ */
+#ifndef KF2VEC_GPU_H
+#define KF2VEC_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KF_ABI_VERSION 1
+
+#define KF_OK 0
+#define KF_EINVAL (-1)   /* bad argument (k out of range, null pointer, ...) */
+#define KF_EHIP (-2)     /* HIP runtime error */
+#define KF_ERANGE (-3)   /* output buffer too small / size overflow */
+#define KF_EFORMAT (-4)  /* unparseable input */
+
+#define KF_MIN_K 2
+#define KF_MAX_K 12      /* device kernels; the CLI accepts 3..11 */
+
+/* kf_count_batch flags */
+#define KF_ACCUMULATE 1u /* do not zero d_counts / d_totals first */
+
+/* input formats */
+#define KF_FMT_AUTO 0    /* sniff: first byte '@' -> FASTQ, else FASTA */
+#define KF_FMT_FASTA 1
+#define KF_FMT_FASTQ 2
+
+int kf_abi_version(void);
+const char* kf_last_error(void);
+
+/* Number of bins (= lines of the reference vocab file for k, main.py:278-296):
+ * 4^k/2 for odd k, (4^k + 4^(k/2))/2 for even k.  0 if k is out of range. */
+uint64_t kf_num_bins(int k);
+
+/* Bin tables for k (replaces the vocab file read, main.py:278-296, and the
+ * dump->vocab left-merge, main.py:323-328):
+ *   code2col[4^k] : kf code of ANY k-mer -> column of its canonical class
+ *   col2rep[nbins]: column -> the kf code the device kernels count it under
+ *                   (min(code, revcomp(code)) in kf-code order)
+ * Either pointer may be NULL.  *nbins receives kf_num_bins(k). */
+int kf_tables(int k, uint32_t* code2col, uint32_t* col2rep, uint64_t* nbins);
+
+/* Sorted canonical vocabulary as text, "KMER\n" per line (byte-identical to the
+ * reference's kf2vec/data files for k=3..9).  cap >= nbins*(k+1). */
+int kf_vocab_text(int k, char* out, uint64_t cap, uint64_t* written);
+
+/* Record index of one FASTA/FASTQ buffer: the byte ranges that are NOT sequence
+ * (FASTA header lines; FASTQ '@' header, '+' and quality lines), as sorted,
+ * disjoint [start, end) pairs offset by `base` (the buffer's position inside the
+ * device batch).  Newlines between sequence lines are not excluded: the device
+ * kernel skips them, so k-mers span line breaks but never records.
+ * out_iv holds cap_pairs pairs; on KF_ERANGE *n_pairs is the count needed. */
+int kf_index_records(const uint8_t* bytes, uint64_t len, int fmt, uint64_t base,
+                     uint64_t* out_iv, uint64_t cap_pairs, uint64_t* n_pairs,
+                     int* fmt_detected);
+
+/* Count canonical k-mers of a batch of genomes already resident in HBM
+ * (replaces `jellyfish count -C` + `jellyfish dump -c`, main.py:309-323).
+ *   d_bytes    : batch bytes, 16-byte aligned; genome g is
+ *                d_bytes[d_goff[g], d_goff[g+1])
+ *   d_goff     : n_genomes+1 non-decreasing offsets (device)
+ *   d_excl     : 2*n_excl sorted disjoint [start,end) pairs (device) from
+ *                kf_index_records, positions absolute in d_bytes (may be NULL if 0)
+ *   d_code2col, d_col2rep : kf_tables(k) uploaded to the device
+ *   d_counts   : n_genomes x nbins uint32 (column order), zeroed first unless
+ *                flags & KF_ACCUMULATE
+ *   d_totals   : n_genomes uint64, number of k-mers counted per genome
+ * Asynchronous on `stream`. */
+int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
+                   const uint64_t* d_excl, uint64_t n_excl,
+                   const uint32_t* d_code2col, const uint32_t* d_col2rep, int k,
+                   uint32_t* d_counts, uint64_t* d_totals, uint32_t flags, void* stream);
+
+/* Grid the count kernel will use on the current device for k (workgroups,
+ * threads per workgroup, dynamic LDS bytes); for roofline accounting. */
+int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
+
+/* Synthetic FASTA generator on the device (benchmark/test input; spec in
+ * DESIGN.md "Synthetic genomes"): genome i has id g = g0 + i*g_stride (so a rank
+ * of a round-robin shard passes g0 = rank, g_stride = world) and seed seed0 + g;
+ * it is written to d_bytes[d_goff[i], d_goff[i+1]) as ">syn_<g>\n" + seq_len
+ * bases in `width`-column lines + '\n' padding.  d_goff must be 16-aligned. */
+int kf_synth_fasta(uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
+                   int64_t g0, int64_t g_stride, uint64_t seed0, uint64_t seq_len,
+                   int width, uint64_t n_period, void* stream);
+
+/* Host-side layout for kf_synth_fasta: genome sizes rounded up to `align`. */
+uint64_t kf_synth_genome_bytes(int64_t g, uint64_t seq_len, int width, uint64_t align);
+uint64_t kf_synth_header_len(int64_t g);
+
+/* One `.kf` line, byte-identical to main.py:331-357:
+ *   "<name>," + ",".join(str(v)) + "\n"
+ * with v = counts (+0.5 if pseudocount) (/ sum unless raw_cnt), float64,
+ * printed like Python repr(float); raw counts with no empty bin print as
+ * integers (pandas keeps int64 when the left-merge introduces no NaN).
+ * On KF_ERANGE *written is the size needed. */
+int kf_format_kf(const char* name, const uint32_t* counts, uint64_t nbins,
+                 int pseudocount, int raw_cnt, char* out, uint64_t cap, uint64_t* written);
+
+/* Format and write many `.kf` files with n_threads host threads:
+ * file i = dir + "/" + names[i] + ".kf", counts row i of counts[n x nbins]. */
+int kf_write_kf_files(const char* dir, const char* const* names, int32_t n,
+                      const uint32_t* counts, uint64_t nbins, int pseudocount,
+                      int raw_cnt, int n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KF2VEC_GPU_H */

@@ -1,0 +1,58 @@
+"""Builds the in-tree HIP library ``kf2vecfsw_amd/libkf2vec_gpu.so`` for gfx950.
+
+``python -m kf2vecfsw_amd.build`` (also called by ``__graft_entry__.build()``).
+hipcc cross-compiles for gfx950 without a GPU; the .so is git-ignored but ships
+to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libkf2vec_gpu.so")
+BUILD = os.path.join(HERE, "_build")
+ARCH = os.environ.get("KF_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES_HIP = ["kf_count.hip"]
+SOURCES_CPP = ["kf_host.cpp"]
+DEPS = SOURCES_HIP + SOURCES_CPP + ["kf_internal.h", "../../include/kf2vec_gpu.h"]
+
+
+def _stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(os.path.join(CSRC, d)) > t for d in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return OUT
+    os.makedirs(BUILD, exist_ok=True)
+    objs = []
+    for s in SOURCES_HIP:
+        o = os.path.join(BUILD, s + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+               "-c", os.path.join(CSRC, s), "-o", o]
+        if verbose:
+            cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
+        subprocess.run(cmd, check=True)
+        objs.append(o)
+    for s in SOURCES_CPP:
+        o = os.path.join(BUILD, s + ".o")
+        subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-pthread",
+                        "-c", os.path.join(CSRC, s), "-o", o], check=True)
+        objs.append(o)
+    tmp = OUT + ".tmp"
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs, "-o", tmp],
+                   check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))

@@ -1,0 +1,265 @@
+"""Host-side driver of the device k-mer counter.
+
+Mirrors the per-file work of kf2vec's ``get_frequencies`` (reference
+kf2vec/main.py:301-357) for a whole batch of genomes at once:
+
+* :func:`pack_genomes` / :func:`pack_files` lay several FASTA/FASTQ files out
+  back to back in one (pinned) host buffer and build the record index
+  (``kf_index_records``) -- the device-side replacement of the ``jellyfish
+  count`` input (main.py:309-311);
+* :class:`KmerCounter` owns the per-k bin tables on the device (the vocab of
+  main.py:278-296) and runs ``kf_count_batch`` on PyTorch-ROCm tensors, giving
+  the ``n_genomes x nbins`` count matrix in vocab column order -- what the
+  reference gets from ``jellyfish dump -c`` + the left-merge (main.py:317-328).
+
+PyTorch is used for device memory and streams only.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import os
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+ALIGN = 16  # genome starts are 16-byte aligned inside a batch ('\n' padding)
+
+
+def num_bins(k: int) -> int:
+    return int(N.lib().kf_num_bins(k))
+
+
+def tables(k: int) -> tuple[np.ndarray, np.ndarray]:
+    """(code2col[4^k], col2rep[nbins]) -- see include/kf2vec_gpu.h kf_tables."""
+    nb = num_bins(k)
+    code2col = np.empty(1 << (2 * k), dtype=np.uint32)
+    col2rep = np.empty(nb, dtype=np.uint32)
+    n = ctypes.c_uint64(0)
+    N.check(N.lib().kf_tables(k, code2col.ctypes.data, col2rep.ctypes.data, ctypes.byref(n)), "kf_tables")
+    assert n.value == nb
+    return code2col, col2rep
+
+
+def vocab_text(k: int) -> bytes:
+    nb = num_bins(k)
+    buf = np.empty(nb * (k + 1), dtype=np.uint8)
+    w = ctypes.c_uint64(0)
+    N.check(N.lib().kf_vocab_text(k, buf.ctypes.data, buf.size, ctypes.byref(w)), "kf_vocab_text")
+    return buf[: w.value].tobytes()
+
+
+def index_records(data: np.ndarray, fmt: int = N.KF_FMT_AUTO, base: int = 0) -> tuple[np.ndarray, int]:
+    """Excluded (non-sequence) byte ranges of one file, as a flat [s0,e0,s1,e1,...]
+    uint64 array offset by ``base``; also returns the detected format."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    cap = 64
+    while True:
+        out = np.empty(2 * cap, dtype=np.uint64)
+        n = ctypes.c_uint64(0)
+        f = ctypes.c_int(0)
+        rc = N.lib().kf_index_records(data.ctypes.data, data.size, fmt, base, out.ctypes.data, cap,
+                                      ctypes.byref(n), ctypes.byref(f))
+        if rc == N.KF_ERANGE:
+            cap = int(n.value)
+            continue
+        N.check(rc, "kf_index_records")
+        return out[: 2 * n.value], int(f.value)
+
+
+@dataclasses.dataclass
+class HostBatch:
+    """Genomes packed back to back: genome g = data[off[g]:off[g+1]]."""
+    data: torch.Tensor          # uint8, (pinned) host
+    off: np.ndarray             # uint64 [n+1]
+    excl: np.ndarray            # uint64 [2*m] absolute [start, end) pairs
+    names: list[str]
+
+    @property
+    def n(self) -> int:
+        return len(self.off) - 1
+
+    def seq_chars(self) -> int:
+        """Sequence characters (excludes header/quality lines and newlines)."""
+        d = self.data.numpy()
+        nl = int(np.count_nonzero(d[: int(self.off[-1])] == 10))
+        ex = int((self.excl[1::2] - self.excl[0::2]).sum()) if self.excl.size else 0
+        return int(self.off[-1] - self.off[0]) - nl - ex
+
+
+def _layout(sizes: Sequence[int]) -> np.ndarray:
+    off = np.zeros(len(sizes) + 1, dtype=np.uint64)
+    pos = 0
+    for i, s in enumerate(sizes):
+        off[i] = pos
+        pos += (int(s) + ALIGN - 1) // ALIGN * ALIGN
+    off[-1] = pos
+    return off
+
+
+def _alloc_host(nbytes: int, pin: bool) -> torch.Tensor:
+    pin = pin and torch.cuda.is_available()
+    return torch.empty(max(nbytes, ALIGN), dtype=torch.uint8, pin_memory=pin)
+
+
+def pack_genomes(blobs: Sequence[bytes | np.ndarray], names: Sequence[str] | None = None,
+                 fmt: int = N.KF_FMT_AUTO, pin: bool = True) -> HostBatch:
+    sizes = [len(b) for b in blobs]
+    off = _layout(sizes)
+    data = _alloc_host(int(off[-1]), pin)
+    d = data.numpy()
+    d[: int(off[-1])] = 10  # '\n' padding between genomes is transparent
+    excl = []
+    for i, b in enumerate(blobs):
+        a = np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray, memoryview)) else np.asarray(b, np.uint8)
+        lo = int(off[i])
+        d[lo: lo + a.size] = a
+        iv, _ = index_records(d[lo: lo + a.size], fmt, lo)
+        excl.append(iv)
+    ex = np.concatenate(excl) if excl else np.zeros(0, np.uint64)
+    return HostBatch(data, off, ex.astype(np.uint64), list(names) if names else [str(i) for i in range(len(blobs))])
+
+
+def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: int = N.KF_FMT_AUTO,
+               pin: bool = True) -> HostBatch:
+    sizes = [os.path.getsize(p) for p in paths]
+    off = _layout(sizes)
+    data = _alloc_host(int(off[-1]), pin)
+    d = data.numpy()
+    excl = []
+    for i, p in enumerate(paths):
+        lo, sz = int(off[i]), sizes[i]
+        with open(p, "rb", buffering=0) as f:
+            got = f.readinto(memoryview(d[lo: lo + sz]))
+        if got != sz:
+            raise IOError(f"short read on {p}")
+        d[lo + sz: int(off[i + 1])] = 10
+        iv, _ = index_records(d[lo: lo + sz], fmt, lo)
+        excl.append(iv)
+    ex = np.concatenate(excl) if excl else np.zeros(0, np.uint64)
+    return HostBatch(data, off, ex.astype(np.uint64), list(names) if names else list(paths))
+
+
+@dataclasses.dataclass
+class DeviceBatch:
+    data: torch.Tensor      # uint8 on device (16-byte aligned)
+    off: torch.Tensor       # int64 [n+1]
+    excl: torch.Tensor      # int64 [2m]
+    n: int
+    n_excl: int
+
+
+def to_device(hb: HostBatch, device: torch.device | str = "cuda") -> DeviceBatch:
+    dev = torch.device(device)
+    data = hb.data.to(dev, non_blocking=True)
+    off = torch.from_numpy(hb.off.view(np.int64)).to(dev, non_blocking=True)
+    ex = hb.excl if hb.excl.size else np.zeros(2, np.uint64)
+    excl = torch.from_numpy(ex.view(np.int64)).to(dev, non_blocking=True)
+    return DeviceBatch(data, off, excl, hb.n, hb.excl.size // 2)
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class KmerCounter:
+    """Canonical k-mer counter for one k on one device (the ``jellyfish count -C
+    -m k`` + ``dump -c`` + vocab merge of main.py:309-328)."""
+
+    def __init__(self, k: int, device: torch.device | str = "cuda"):
+        if not (N.KF_MIN_K <= k <= N.KF_MAX_K):
+            raise ValueError(f"k={k} out of range [{N.KF_MIN_K}, {N.KF_MAX_K}]")
+        self.k = k
+        self.device = torch.device(device)
+        if self.device.type != "cuda" or not torch.cuda.is_available():
+            raise N.NativeError("KmerCounter needs a ROCm GPU (no CPU fallback)")
+        self.nbins = num_bins(k)
+        c2c, c2r = tables(k)
+        self.code2col = torch.from_numpy(c2c.view(np.int32)).to(self.device)
+        self.col2rep = torch.from_numpy(c2r.view(np.int32)).to(self.device)
+
+    def launch_info(self) -> tuple[int, int, int]:
+        g, b, l = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        with torch.cuda.device(self.device):
+            N.check(N.lib().kf_count_launch_info(self.k, ctypes.byref(g), ctypes.byref(b), ctypes.byref(l)),
+                    "kf_count_launch_info")
+        return g.value, b.value, l.value
+
+    def alloc_out(self, n: int) -> tuple[torch.Tensor, torch.Tensor]:
+        return (torch.empty((n, self.nbins), dtype=torch.int32, device=self.device),
+                torch.empty(n, dtype=torch.int64, device=self.device))
+
+    def count(self, db: DeviceBatch, counts: torch.Tensor | None = None, totals: torch.Tensor | None = None,
+              accumulate: bool = False, stream: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+        """Enqueue the count kernel; returns (counts int32[n, nbins] holding uint32
+        bit patterns, totals int64[n]) on the device."""
+        if counts is None or totals is None:
+            counts, totals = self.alloc_out(db.n)
+        assert counts.shape == (db.n, self.nbins) and counts.dtype == torch.int32 and counts.is_contiguous()
+        assert totals.shape == (db.n,) and totals.dtype == torch.int64
+        assert db.data.data_ptr() % 16 == 0
+        s = _stream_ptr(self.device) if stream is None else stream
+        with torch.cuda.device(self.device):
+            N.check(N.lib().kf_count_batch(
+                db.data.data_ptr(), db.off.data_ptr(), db.n, db.excl.data_ptr() if db.n_excl else None,
+                db.n_excl, self.code2col.data_ptr(), self.col2rep.data_ptr(), self.k,
+                counts.data_ptr(), totals.data_ptr(), N.KF_ACCUMULATE if accumulate else 0, s), "kf_count_batch")
+        return counts, totals
+
+
+def counts_to_numpy(counts: torch.Tensor) -> np.ndarray:
+    return counts.cpu().numpy().view(np.uint32)
+
+
+def synth_ids(n: int, g0: int = 0, g_stride: int = 1) -> list[int]:
+    return [g0 + i * g_stride for i in range(n)]
+
+
+def synth_layout(n: int, seq_len: int, width: int = 80, g0: int = 0, g_stride: int = 1,
+                 align: int = 256) -> np.ndarray:
+    """Offsets of n synthetic genomes (kf_synth_fasta layout)."""
+    L = N.lib()
+    off = np.zeros(n + 1, dtype=np.uint64)
+    pos = 0
+    for i, g in enumerate(synth_ids(n, g0, g_stride)):
+        off[i] = pos
+        pos += int(L.kf_synth_genome_bytes(g, seq_len, width, align))
+    off[-1] = pos
+    return off
+
+
+def synth_excl(off: np.ndarray, g0: int = 0, g_stride: int = 1) -> np.ndarray:
+    """Record index of a synthetic batch: one header line per genome."""
+    L = N.lib()
+    n = len(off) - 1
+    ex = np.empty(2 * n, dtype=np.uint64)
+    for i, g in enumerate(synth_ids(n, g0, g_stride)):
+        ex[2 * i] = off[i]
+        ex[2 * i + 1] = off[i] + int(L.kf_synth_header_len(g)) - 1  # up to the header's '\n'
+    return ex
+
+
+def synth_fasta_bytes(seq_len: int, width: int = 80, g: int = 0) -> int:
+    """Unpadded FASTA size of one synthetic genome (header + bases + newlines)."""
+    return int(N.lib().kf_synth_header_len(g)) + seq_len + (seq_len + width - 1) // width
+
+
+def synth_device_batch(n: int, seq_len: int, seed0: int, width: int = 80, n_period: int = 0, g0: int = 0,
+                       g_stride: int = 1, device: torch.device | str = "cuda") -> DeviceBatch:
+    """Generate n synthetic FASTA genomes (ids g0 + i*g_stride) directly in HBM."""
+    dev = torch.device(device)
+    off = synth_layout(n, seq_len, width, g0, g_stride)
+    ex = synth_excl(off, g0, g_stride)
+    data = torch.empty(int(off[-1]), dtype=torch.uint8, device=dev)
+    doff = torch.from_numpy(off.view(np.int64)).to(dev)
+    dex = torch.from_numpy(ex.view(np.int64)).to(dev)
+    s = _stream_ptr(dev)
+    with torch.cuda.device(dev):
+        for c0 in range(0, n, 65535):
+            c1 = min(n, c0 + 65535)
+            N.check(N.lib().kf_synth_fasta(data.data_ptr(), doff[c0:].data_ptr(), c1 - c0, g0 + c0 * g_stride,
+                                           g_stride, seed0, seq_len, width, n_period, s), "kf_synth_fasta")
+    return DeviceBatch(data, doff, dex, n, n)

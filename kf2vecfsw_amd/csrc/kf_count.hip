@@ -1,0 +1,666 @@
+// kf_count.hip -- canonical k-mer counting kernels for MI355X (gfx950, CDNA4).
+//
+// Replaces the Jellyfish shell-out of kf2vec's get_frequencies
+// (reference kf2vec/main.py:309-323: `jellyfish count -C` + `jellyfish dump -c`
+// + the pandas read of the dump).  Semantics restated in oracle/kmer_oracle.c.
+//
+// Work decomposition (DESIGN.md "Kernel K1"):
+//   * the batch [goff[0], goff[n)) is split into `gridDim.x` equal byte spans, one
+//     per workgroup (512 threads = 8 waves); a span may cross genome boundaries;
+//   * each genome piece of a span is split into 8 contiguous wave ranges; a wave
+//     walks its range in 1 KiB chunks, lane L owning bytes [16L, 16L+16) of the
+//     chunk (one coalesced dwordx4 per lane, 3 chunks prefetched);
+//   * per lane: SWAR classification of the 16 bytes (v_perm + v_dot4, no table
+//     loads), newline compaction, then the k-1 bases of context arrive from
+//     lane L-1 through one DPP `wave_shr:1` (lane 0 from the previous chunk's
+//     lane 63); the 16 k-mer windows are cut from a 64-bit register window by
+//     v_bfe, canonicalised by min(fwd, revcomp) and counted with one LDS
+//     `ds_add_u32` each into the workgroup's 4^k-entry histogram (k <= 7);
+//   * at the end of a genome piece the histogram is flushed with coalesced u32
+//     global atomics in column order (col2rep gather) and re-zeroed;
+//   * k >= 8: the same front end, counting straight into global memory.
+// Records: FASTA header / FASTQ non-sequence lines arrive as an interval list
+// (kf_index_records) and are treated as invalid bytes (k-mer reset).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kf_internal.h"
+
+namespace kf {
+
+constexpr int kWave = 64;
+constexpr int kChunk = 1024;       // bytes per wave iteration (64 lanes x 16 B)
+constexpr int kBlock = 512;        // threads per workgroup
+constexpr int kWaves = kBlock / kWave;
+constexpr int kLdsMaxK = 7;        // 4^7 x 4 B = 64 KiB histogram
+
+struct CountArgs {
+    const uint8_t* bytes;
+    const uint64_t* goff;
+    const uint64_t* excl;          // [s0,e0,s1,e1,...]
+    uint64_t n_excl;
+    const uint32_t* code2col;
+    const uint32_t* col2rep;
+    uint32_t* counts;
+    unsigned long long* totals;
+    uint32_t nbins;
+    int32_t n_genomes;
+};
+
+// ---------------------------------------------------------------- tails
+// A "tail" summarises a stretch of the compacted entry stream:
+//   codes [0,22): the last <= k-1 entries' 2-bit codes (last entry lowest)
+//   n     [22,27): length of the trailing run of valid bases (capped at 31)
+//   ne    [27,32): number of entries (capped at 31)
+__device__ __forceinline__ uint32_t tail_pack(uint32_t codes, uint32_t n, uint32_t ne) {
+    return codes | (min(n, 31u) << 22) | (min(ne, 31u) << 27);
+}
+__device__ __forceinline__ uint32_t t_codes(uint32_t t) { return t & 0x3FFFFFu; }
+__device__ __forceinline__ uint32_t t_n(uint32_t t) { return (t >> 22) & 31u; }
+__device__ __forceinline__ uint32_t t_ne(uint32_t t) { return t >> 27; }
+
+template <int K>
+__device__ __forceinline__ uint32_t tail_combine(uint32_t a, uint32_t b) {
+    constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
+    const uint32_t bn = t_n(b), bne = t_ne(b);
+    const uint32_t n = (bn < bne) ? bn : min(t_n(a) + bn, 31u);
+    const uint32_t codes =
+        (bne >= (uint32_t)(K - 1)) ? t_codes(b) : (((t_codes(a) << (2 * bne)) | t_codes(b)) & TM);
+    return tail_pack(codes, n, t_ne(a) + bne);
+}
+template <int K>
+__device__ __forceinline__ bool tail_complete(uint32_t t) {
+    return t_n(t) < t_ne(t) || t_n(t) >= (uint32_t)(K - 1);
+}
+
+// ---------------------------------------------------------------- classify
+// 16 bytes -> codes C (byte i at bits 2(15-i)), invalid mask INV and newline
+// mask NL (byte i at bit 15-i).  Valid bases: ACGTacgt.
+//   cb = (b >> 1) & 3            kf code (A0 C1 T2 G3)
+//   y  = (b ^ TBL[cb]) & 0xDF    == 0x0C iff b is the base cb (either case)
+//   perm(-1,-1,sel) yields 0x00 for sel == 12 and 0xFF for every other byte
+//   dot4 packs four codes / four flags into one byte / nibble in memory order.
+__device__ __forceinline__ void classify16(const uint4 d, uint32_t& C, uint32_t& INV, uint32_t& NL) {
+    const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+    uint32_t pc[4];
+    int pv[4], pn[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = w[q];
+        const uint32_t cb = (x >> 1) & 0x03030303u;
+        const uint32_t ex = __builtin_amdgcn_perm(0u, 0x4B584F4Du, cb);   // "ACTG" ^ 0x0C
+        const uint32_t y = (x ^ ex) & 0xDFDFDFDFu;
+        const uint32_t vf = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, y);
+        const uint32_t nf = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, x ^ 0x06060606u);
+        pc[q] = __builtin_amdgcn_udot4(cb, 0x01041040u, 0u, false);
+        pv[q] = __builtin_amdgcn_sdot4((int)vf, 0x01020408, 0, false);
+        pn[q] = __builtin_amdgcn_sdot4((int)nf, 0x01020408, 0, false);
+    }
+    C = (pc[0] << 24) | (pc[1] << 16) | (pc[2] << 8) | pc[3];
+    // pv/pn are minus the flag nibbles; sum them modulo 2^32 and negate once
+    INV = 0u - (((uint32_t)pv[0] << 12) + ((uint32_t)pv[1] << 8) + ((uint32_t)pv[2] << 4) + (uint32_t)pv[3]);
+    NL = 0xFFFFu & ~(0u - (((uint32_t)pn[0] << 12) + ((uint32_t)pn[1] << 8) + ((uint32_t)pn[2] << 4) +
+                           (uint32_t)pn[3]));
+}
+
+// Remove newline entries (compaction).  C: 2-bit entries, V/EN: 1-bit masks.
+template <bool MASKED>
+__device__ __forceinline__ void compact(uint32_t nl, uint32_t& C, uint32_t& V, uint32_t& EN) {
+    while (nl) {
+        const uint32_t r = __builtin_ctz(nl);
+        const uint32_t lo1 = (1u << r) - 1u;
+        V = ((V >> (r + 1)) << r) | (V & lo1);
+        if (MASKED) EN = ((EN >> (r + 1)) << r) | (EN & lo1);
+        const uint32_t lo2 = (1u << (2 * r)) - 1u;
+        C = (((C >> (2 * r + 1)) >> 1) << (2 * r)) | (C & lo2);
+        nl = (nl >> (r + 1)) << r;
+    }
+}
+
+__device__ __forceinline__ uint32_t revpairs(uint32_t x) {
+    const uint32_t t = __builtin_bitreverse32(x);
+    return ((t << 1) & 0xAAAAAAAAu) | ((t >> 1) & 0x55555555u);
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t run_mask(uint32_t E) {
+    // bit r set iff entries r .. r+K-1 are all valid
+    uint32_t R = E;
+    int a = 1;
+#pragma unroll
+    for (int it = 0; it < 5; ++it) {
+        if (a < K) {
+            const int s = (a < K - a) ? a : (K - a);
+            R &= R >> s;
+            a += s;
+        }
+    }
+    return R;
+}
+
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+// Exclusive scan of lane tails with a carry-in (slow path: some lane's block has
+// fewer than k-1 entries and no reset, e.g. very short FASTA lines).
+template <int K>
+__device__ __noinline__ uint32_t scan_ctx(uint32_t own, uint32_t carry, int lane) {
+    uint32_t v = own;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d, kWave);
+        if (lane >= d) v = tail_combine<K>(o, v);
+    }
+    const uint32_t ex = __shfl_up(v, 1, kWave);
+    return lane == 0 ? carry : tail_combine<K>(carry, ex);
+}
+
+// Load a wave-uniform 64-bit word and pin it in SGPRs: compares against it then
+// never wait on the vector-memory counter shared with the byte-stream prefetch.
+__device__ __forceinline__ uint64_t uload64(const uint64_t* p) {
+    const uint64_t v = *p;
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
+struct ChunkMask {
+    // byte-position bounds for masked chunks (absolute offsets)
+    uint64_t glo;   // bytes < glo are invalid (previous genome)
+    uint64_t lo;    // count only windows ending at bytes in [lo, hi)
+    uint64_t hi;
+};
+
+__device__ __forceinline__ uint32_t range_bits(int64_t a, int64_t b) {
+    // bits for bytes [a, b) of a 16-byte block (byte i at bit 15-i), a,b clamped to [0,16]
+    a = a < 0 ? 0 : (a > 16 ? 16 : a);
+    b = b < 0 ? 0 : (b > 16 ? 16 : b);
+    if (b <= a) return 0u;
+    const uint32_t n = (uint32_t)(b - a);
+    return ((n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << (16 - (uint32_t)b)) & 0xFFFFu;
+}
+
+// Apply genome start / count window / excluded intervals to one lane's block.
+__device__ __forceinline__ void apply_masks(const CountArgs& A, uint64_t chunk, int lane,
+                                            const ChunkMask& m, uint64_t iv0,
+                                            uint32_t& INV, uint32_t& EN) {
+    const int64_t b0 = (int64_t)(chunk + 16u * (uint32_t)lane);
+    INV |= range_bits(-1, (int64_t)m.glo - b0);
+    EN = range_bits((int64_t)m.lo - b0, (int64_t)m.hi - b0);
+    const uint64_t cend = chunk + kChunk;
+    for (uint64_t i = iv0; i < A.n_excl; ++i) {      // wave-uniform loop
+        const uint64_t s = uload64(A.excl + 2 * i), e = uload64(A.excl + 2 * i + 1);
+        if (s >= cend) break;
+        INV |= range_bits((int64_t)s - b0, (int64_t)e - b0);
+    }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const uint8_t* bytes, uint64_t c, uint64_t ghi) {
+    const uint32_t rec = c >= ghi ? 0u : (uint32_t)min<uint64_t>(ghi - c, (uint64_t)kChunk);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c), (short)0, (int)rec, 0x00020000);
+}
+
+__device__ __forceinline__ uint4 load_chunk(const uint8_t* bytes, uint64_t c, uint64_t ghi, int lane) {
+    const auto rs = chunk_rsrc(bytes, c, ghi);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// Per-lane front end shared by every path: block -> (C, V, EN, ne, own tail).
+template <int K, bool MASKED>
+__device__ __forceinline__ void front_end(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
+                                          const ChunkMask& m, uint64_t iv0,
+                                          uint32_t& C, uint32_t& V, uint32_t& EN, uint32_t& ne,
+                                          uint32_t& own) {
+    constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
+    uint32_t INV, NL;
+    classify16(d, C, INV, NL);
+    EN = 0xFFFFu;
+    if (MASKED) apply_masks(A, chunk, lane, m, iv0, INV, EN);
+    V = ~INV & 0xFFFFu;
+    ne = 16u - (uint32_t)__builtin_popcount(NL);
+    compact<MASKED>(NL, C, V, EN);
+    const uint32_t n = min((uint32_t)__builtin_ctz(~V), ne);
+    own = tail_pack(C & TM, n, ne);
+}
+
+// Inclusive tail of the 1 KiB chunk starting at p (warm-up only; p may lie
+// before glo or even before the buffer: those bytes read as invalid).
+template <int K>
+__device__ __noinline__ uint32_t chunk_tail(const uint8_t* bytes, const uint64_t* excl, uint64_t n_excl, int64_t p,
+                                            uint64_t glo, int lane) {
+    CountArgs A{};
+    A.bytes = bytes;
+    A.excl = excl;
+    A.n_excl = n_excl;
+    const int64_t b0 = p + 16 * lane;
+    uint4 d = make_uint4(0u, 0u, 0u, 0u);
+    if (b0 >= (int64_t)(glo & ~(uint64_t)15)) d = *(const uint4*)(A.bytes + b0);
+    // first excluded interval that ends after the chunk start (binary search)
+    const uint64_t key = p < 0 ? 0 : (uint64_t)p;
+    uint64_t lo = 0, hi = A.n_excl;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (A.excl[2 * mid + 1] <= key) lo = mid + 1; else hi = mid;
+    }
+    ChunkMask m{glo, 0, 0};
+    uint32_t C, V, EN, ne, own;
+    front_end<K, true>(d, A, (uint64_t)p, lane, m, lo, C, V, EN, ne, own);
+    uint32_t v = own;
+#pragma unroll
+    for (int dd = 1; dd < kWave; dd <<= 1) {
+        const uint32_t o = __shfl_up(v, dd, kWave);
+        if (lane >= dd) v = tail_combine<K>(o, v);
+    }
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, kWave - 1);
+}
+
+// Count one chunk.  GLOBAL = count straight into d_counts (k > kLdsMaxK).
+template <int K, bool MASKED, bool GLOBAL>
+__device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
+                                                const ChunkMask& m, uint64_t iv0, uint32_t carry,
+                                                uint32_t* __restrict__ hist, uint32_t* __restrict__ gcounts,
+                                                uint32_t& lane_total) {
+    constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
+    constexpr int W2 = 2 * K;
+    uint32_t C, V, EN, ne, own;
+    front_end<K, MASKED>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
+
+    // context = own tail of lane L-1 (lane 0: carry), exact unless some lane is incomplete
+    uint32_t ctx = wave_shr1(carry, own);
+    const uint64_t inc_mask = __ballot(!tail_complete<K>(own)) & 0x7FFFFFFFFFFFFFFFull;
+    if (inc_mask) ctx = scan_ctx<K>(own, carry, lane);
+
+    const uint32_t ctxlen = min(t_n(ctx), (uint32_t)(K - 1));
+    const uint64_t W = ((uint64_t)t_codes(ctx) << (2 * ne)) | (uint64_t)C;
+    const uint32_t E = (((1u << ctxlen) - 1u) << ne) | V;
+    uint32_t R = run_mask<K>(E) & ((1u << ne) - 1u);
+    if (MASKED) R &= EN;
+
+    const uint32_t wlo = (uint32_t)W, whi = (uint32_t)(W >> 32);
+    const uint32_t rhi = revpairs(wlo) ^ 0xAAAAAAAAu;   // revcomp of the 64-bit window
+    const uint32_t rlo = revpairs(whi) ^ 0xAAAAAAAAu;
+    constexpr int RS = 2 * (17 - K);
+    const uint32_t rplo = __builtin_amdgcn_alignbit(rhi, rlo, RS);
+    const uint32_t rphi = rhi >> RS;
+    const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
+                            __builtin_amdgcn_alignbit(whi, wlo, 24)};
+    const uint32_t rv[4] = {rplo, __builtin_amdgcn_alignbit(rphi, rplo, 8),
+                            __builtin_amdgcn_alignbit(rphi, rplo, 16), __builtin_amdgcn_alignbit(rphi, rplo, 24)};
+    if (!GLOBAL) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int fo = (2 * r) & ~7;
+            const uint32_t f = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, W2);
+            const int rr = 2 * (15 - r), ro = rr & ~7;
+            const uint32_t c = __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, W2);
+            const uint32_t inc = (R >> r) & 1u;
+            __hip_atomic_fetch_add(hist + min(f, c), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int fo = (2 * r) & ~7;
+            const uint32_t f = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, W2);
+            const int rr = 2 * (15 - r), ro = rr & ~7;
+            const uint32_t c = __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, W2);
+            if ((R >> r) & 1u) {
+                const uint32_t col = A.code2col[min(f, c)];
+                __hip_atomic_fetch_add(gcounts + col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    lane_total += (uint32_t)__builtin_popcount(R);
+    // inclusive tail of lane 63 = next chunk's carry
+    const uint32_t incl = tail_pack(wlo & TM, (uint32_t)__builtin_ctz(~E), 31u);
+    return (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+}
+
+// Process the wave range [lo, hi) of genome [glo, ghi).
+template <int K, bool GLOBAL>
+__device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
+                                                  uint64_t lo, uint64_t hi, int lane,
+                                                  uint32_t* __restrict__ hist) {
+    uint64_t c = lo & ~(uint64_t)15;
+    if (lo >= hi) return 0;
+    uint32_t* gcounts = GLOBAL ? A.counts + (uint64_t)g * A.nbins : nullptr;
+
+    // warm-up: exact k-1 context before c (walk back until complete)
+    uint32_t carry = tail_pack(0, 0, 0);
+    {
+        int64_t p = (int64_t)c;
+        while (p > (int64_t)glo && !tail_complete<K>(carry)) {
+            p -= kChunk;
+            carry = tail_combine<K>(chunk_tail<K>(A.bytes, A.excl, A.n_excl, p, glo, lane), carry);
+        }
+    }
+    // first excluded interval ending after c; its bounds live in registers so the
+    // chunk loop issues no vector loads besides the byte stream (a VMEM load there
+    // would force vmcnt(0) and drain the prefetch ring)
+    uint64_t iv = 0;
+    {
+        uint64_t a = 0, b = A.n_excl;
+        while (a < b) {
+            const uint64_t mid = (a + b) >> 1;
+            if (uload64(A.excl + 2 * mid + 1) <= c) a = mid + 1; else b = mid;
+        }
+        iv = a;
+    }
+    uint64_t iv_s = ~0ull, iv_e = ~0ull;
+    if (iv < A.n_excl) {
+        iv_s = uload64(A.excl + 2 * iv);
+        iv_e = uload64(A.excl + 2 * iv + 1);
+    }
+    const ChunkMask m{glo, lo, hi};
+    uint32_t lane_total = 0;
+    // 4-deep ring, 3 chunks in flight while one is counted; a buffer is refilled
+    // only after it has been consumed, so no register rotation waits on a load
+    uint4 b0 = load_chunk(A.bytes, c, ghi, lane);
+    uint4 b1 = load_chunk(A.bytes, c + kChunk, ghi, lane);
+    uint4 b2 = load_chunk(A.bytes, c + 2 * kChunk, ghi, lane);
+    uint4 b3 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+    auto count = [&](const uint4 buf) {
+        if (c >= iv_e) {   // passed the current interval (rare)
+            do { ++iv; } while (iv < A.n_excl && uload64(A.excl + 2 * iv + 1) <= c);
+            iv_s = iv < A.n_excl ? uload64(A.excl + 2 * iv) : ~0ull;
+            iv_e = iv < A.n_excl ? uload64(A.excl + 2 * iv + 1) : ~0ull;
+        }
+        const bool has_iv = iv_s < c + kChunk;
+        const bool edge = c < lo || c + kChunk > hi;
+        if (edge || has_iv)
+            carry = count_chunk<K, true, GLOBAL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total);
+        else
+            carry = count_chunk<K, false, GLOBAL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total);
+        c += kChunk;
+    };
+    // steady state: groups of 4 chunks with no exit in between (keeps the
+    // compiler's vmcnt bookkeeping exact: wait for the oldest load only)
+    const uint64_t nch = (hi - c + kChunk - 1) / kChunk;
+    for (uint64_t i = 0; i + 4 <= nch; i += 4) {
+        count(b0);
+        b0 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+        count(b1);
+        b1 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+        count(b2);
+        b2 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+        count(b3);
+        b3 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+    }
+    const uint64_t rem = nch & 3;
+    if (rem > 0) count(b0);
+    if (rem > 1) count(b1);
+    if (rem > 2) count(b2);
+    return lane_total;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, kWave);
+    return v;
+}
+
+template <int K>
+__global__ void __launch_bounds__(kBlock) count_kernel(CountArgs A) {
+    constexpr bool GLOBAL = K > kLdsMaxK;
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr uint32_t NCODES = 1u << (2 * (GLOBAL ? 1 : K));
+    if (!GLOBAL) {
+        for (uint32_t i = tid; i < NCODES; i += kBlock) hist[i] = 0;
+        __syncthreads();
+    }
+    __shared__ unsigned long long red[kWaves];
+
+    const uint64_t base = A.goff[0];
+    const uint64_t total = A.goff[A.n_genomes] - base;
+    const uint64_t G = gridDim.x, b = blockIdx.x;
+    const uint64_t span_lo = base + ((total / G * b + (total % G) * b / G) & ~(uint64_t)15);
+    const uint64_t span_hi = (b + 1 == G) ? base + total
+                                          : base + ((total / G * (b + 1) + (total % G) * (b + 1) / G) & ~(uint64_t)15);
+    if (span_lo >= span_hi) return;
+    // first genome whose end is beyond span_lo
+    int32_t g;
+    {
+        int32_t a = 0, e = A.n_genomes;
+        while (a < e) {
+            const int32_t mid = (a + e) >> 1;
+            if (A.goff[mid + 1] <= span_lo) a = mid + 1; else e = mid;
+        }
+        g = a;
+    }
+    for (; g < A.n_genomes; ++g) {
+        const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
+        if (glo >= span_hi) break;
+        const uint64_t plo = max(glo, span_lo), phi = min(ghi, span_hi);
+        if (phi <= plo) continue;
+        // wave w owns [split(w), split(w+1)): 16-byte aligned, monotone, covering [plo, phi)
+        const uint64_t len = phi - plo;
+        auto split = [&](uint64_t w) -> uint64_t {
+            if (w == 0) return plo;
+            if (w >= (uint64_t)kWaves) return phi;
+            const uint64_t s = (plo + len / kWaves * w + (len % kWaves) * w / kWaves) & ~(uint64_t)15;
+            return min(max(s, plo), phi);
+        };
+        const uint64_t lo_c = split(wave), hi_c = split(wave + 1);
+        const uint64_t lt = process_range<K, GLOBAL>(A, g, glo, ghi, lo_c, hi_c, lane, hist);
+        if (GLOBAL) {
+            const unsigned long long s = wave_sum(lt);
+            if (lane == 0 && s) atomicAdd(A.totals + g, s);
+        } else {
+            __syncthreads();
+            unsigned long long s = 0;
+            uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
+            for (uint32_t col = tid; col < A.nbins; col += kBlock) {
+                const uint32_t rep = A.col2rep[col];
+                const uint32_t v = hist[rep];
+                if (v) {
+                    __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    hist[rep] = 0;
+                    s += v;
+                }
+            }
+            s = wave_sum(s);
+            if (lane == 0) red[wave] = s;
+            __syncthreads();
+            if (tid == 0) {
+                unsigned long long t = 0;
+                for (int w = 0; w < kWaves; ++w) t += red[w];
+                if (t) atomicAdd(A.totals + g, t);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- synthetic input
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ bool in_nrun(uint64_t key, uint64_t i, uint64_t n_period) {
+    if (!n_period) return false;
+    uint64_t b = i >> 12;
+    for (int d = 0; d < 2; ++d) {
+        if (d == 1) {
+            if (b == 0) break;
+            b -= 1;
+        }
+        const uint64_t h = splitmix64((key ^ 0xA5A5A5A5A5A5A5A5ull) + b);
+        if (h % n_period) continue;
+        const uint64_t st = (b << 12) + ((h >> 16) % 4096), ln = 1 + ((h >> 32) % 100);
+        if (i >= st && i < st + ln) return true;
+    }
+    return false;
+}
+
+__global__ void __launch_bounds__(256) synth_kernel(uint8_t* bytes, const uint64_t* goff, int64_t g0, int64_t gstride,
+                                                     uint64_t seed0, uint64_t seq_len, int width, uint64_t n_period) {
+    const int32_t gi = blockIdx.y;
+    const uint64_t lo = goff[gi], hi = goff[gi + 1];
+    const int64_t g = g0 + gi * gstride;
+    // header ">syn_<g>\n"
+    char digits[24];
+    int nd = 0;
+    {
+        uint64_t v = (uint64_t)(g < 0 ? -g : g);
+        do { digits[nd++] = (char)('0' + v % 10); v /= 10; } while (v);
+    }
+    const uint64_t hlen = 5 + (uint64_t)nd + (g < 0 ? 1 : 0) + 1;
+    const uint64_t key = splitmix64(seed0 + (uint64_t)g);
+    const uint64_t W1 = (uint64_t)width + 1;
+    for (uint64_t p0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; lo + p0 < hi;
+         p0 += (uint64_t)gridDim.x * blockDim.x * 16) {
+        uint32_t out[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t p = p0 + j;
+            uint32_t ch;
+            if (p < hlen) {
+                if (p == 0) ch = '>';
+                else if (p < 5) ch = "syn_"[p - 1];
+                else if (g < 0 && p == 5) ch = '-';
+                else if (p == hlen - 1) ch = '\n';
+                else ch = (uint32_t)digits[nd - 1 - (int)(p - 5 - (g < 0 ? 1 : 0))];
+            } else {
+                const uint64_t q = p - hlen, line = q / W1, col = q % W1;
+                const uint64_t i = line * (uint64_t)width + col;
+                if (col == (uint64_t)width || i >= seq_len) {
+                    ch = '\n';
+                } else {
+                    const uint64_t h = splitmix64(key + (i >> 5));
+                    ch = (uint32_t)"ACGT"[(h >> (2 * (i & 31))) & 3];
+                    if (in_nrun(key, i, n_period)) ch = 'N';
+                }
+            }
+            out[j >> 2] |= ch << (8 * (j & 3));
+        }
+        if (lo + p0 + 16 <= hi) {
+            *(uint4*)(bytes + lo + p0) = make_uint4(out[0], out[1], out[2], out[3]);
+        } else {
+            for (int j = 0; lo + p0 + j < hi; ++j) bytes[lo + p0 + j] = (uint8_t)(out[j >> 2] >> (8 * (j & 3)));
+        }
+    }
+}
+
+}  // namespace kf
+
+// ====================================================================== C-ABI
+using namespace kf;
+
+namespace {
+typedef void (*count_fn_t)(CountArgs);
+
+template <int K>
+void* kernel_ptr() { return (void*)&count_kernel<K>; }
+
+void* count_kernel_for(int k) {
+    switch (k) {
+    case 2: return kernel_ptr<2>();
+    case 3: return kernel_ptr<3>();
+    case 4: return kernel_ptr<4>();
+    case 5: return kernel_ptr<5>();
+    case 6: return kernel_ptr<6>();
+    case 7: return kernel_ptr<7>();
+    case 8: return kernel_ptr<8>();
+    case 9: return kernel_ptr<9>();
+    case 10: return kernel_ptr<10>();
+    case 11: return kernel_ptr<11>();
+    case 12: return kernel_ptr<12>();
+    default: return nullptr;
+    }
+}
+
+int lds_bytes_for(int k) { return k <= kLdsMaxK ? (int)(sizeof(uint32_t) << (2 * k)) : 0; }
+
+struct LaunchCache {
+    int grid[KF_MAX_K + 1][64];
+};
+LaunchCache g_cache = {};
+std::mutex g_cache_mu;
+
+int launch_info(int k, int* grid, int* block, int* lds) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
+    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
+    const int l = lds_bytes_for(k);
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    int& gr = g_cache.grid[k][dev];
+    if (!gr) {
+        void* fn = count_kernel_for(k);
+        if (l > 0 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, l) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, l) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipOccupancyMaxActiveBlocksPerMultiprocessor failed");
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipDeviceGetAttribute(MultiprocessorCount) failed");
+        if (per_cu < 1) per_cu = 1;
+        gr = per_cu * cus;
+    }
+    *grid = gr;
+    *block = kBlock;
+    *lds = l;
+    return KF_OK;
+}
+}  // namespace
+
+extern "C" int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes) {
+    if (k < KF_MIN_K || k > KF_MAX_K) return kf_fail(KF_EINVAL, "k out of range [2, 12]");
+    if (!grid || !block || !lds_bytes) return kf_fail(KF_EINVAL, "null output pointer");
+    return launch_info(k, grid, block, lds_bytes);
+}
+
+extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
+                              const uint64_t* d_excl, uint64_t n_excl, const uint32_t* d_code2col,
+                              const uint32_t* d_col2rep, int k, uint32_t* d_counts, uint64_t* d_totals,
+                              uint32_t flags, void* stream) {
+    if (k < KF_MIN_K || k > KF_MAX_K) return kf_fail(KF_EINVAL, "k out of range [2, 12]");
+    if (n_genomes < 0) return kf_fail(KF_EINVAL, "n_genomes < 0");
+    if (n_genomes == 0) return KF_OK;
+    if (!d_bytes || !d_goff || !d_counts || !d_totals || !d_code2col || !d_col2rep)
+        return kf_fail(KF_EINVAL, "null device pointer");
+    if (n_excl && !d_excl) return kf_fail(KF_EINVAL, "d_excl is null but n_excl > 0");
+    if (((uintptr_t)d_bytes) & 15) return kf_fail(KF_EINVAL, "d_bytes must be 16-byte aligned");
+    const uint64_t nb = kf_num_bins(k);
+    hipStream_t s = (hipStream_t)stream;
+    if (!(flags & KF_ACCUMULATE)) {
+        if (hipMemsetAsync(d_counts, 0, (size_t)n_genomes * nb * sizeof(uint32_t), s) != hipSuccess ||
+            hipMemsetAsync(d_totals, 0, (size_t)n_genomes * sizeof(uint64_t), s) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipMemsetAsync failed");
+    }
+    int grid = 0, block = 0, lds = 0;
+    int rc = launch_info(k, &grid, &block, &lds);
+    if (rc) return rc;
+    CountArgs A;
+    A.bytes = d_bytes;
+    A.goff = d_goff;
+    A.excl = d_excl;
+    A.n_excl = n_excl;
+    A.code2col = d_code2col;
+    A.col2rep = d_col2rep;
+    A.counts = d_counts;
+    A.totals = (unsigned long long*)d_totals;
+    A.nbins = (uint32_t)nb;
+    A.n_genomes = n_genomes;
+    void* args[] = {&A};
+    if (hipLaunchKernel(count_kernel_for(k), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
+        return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return KF_OK;
+}
+
+extern "C" int kf_synth_fasta(uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes, int64_t g0,
+                              int64_t g_stride, uint64_t seed0, uint64_t seq_len, int width, uint64_t n_period,
+                              void* stream) {
+    if (n_genomes <= 0) return n_genomes == 0 ? KF_OK : kf_fail(KF_EINVAL, "n_genomes < 0");
+    if (!d_bytes || !d_goff) return kf_fail(KF_EINVAL, "null device pointer");
+    if (width < 1) return kf_fail(KF_EINVAL, "width < 1");
+    if (n_genomes > 65535) return kf_fail(KF_EINVAL, "at most 65535 genomes per synth call");
+    dim3 grid(512, (unsigned)n_genomes);
+    hipLaunchKernelGGL(synth_kernel, grid, dim3(256), 0, (hipStream_t)stream, d_bytes, d_goff, g0, g_stride, seed0,
+                       seq_len, width, n_period);
+    if (hipGetLastError() != hipSuccess) return kf_fail(KF_EHIP, "synth kernel launch failed");
+    return KF_OK;
+}

@@ -1,0 +1,337 @@
+// kf_host.cpp -- host half of the kf2vec_gpu C-ABI (include/kf2vec_gpu.h):
+// bin tables / vocabulary, FASTA/FASTQ record index, byte-exact `.kf` formatting
+// and the parallel `.kf` writer.
+#include <algorithm>
+#include <atomic>
+#include <charconv>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kf_internal.h"
+
+namespace {
+thread_local std::string g_err;
+
+inline uint64_t kf_rc(uint64_t x, int k) {
+    // reverse complement in kf code (complement = ^2)
+    uint64_t r = 0;
+    for (int i = 0; i < k; ++i) {
+        r = (r << 2) | ((x & 3u) ^ 2u);
+        x >>= 2;
+    }
+    return r;
+}
+// kf code (A0 C1 T2 G3) -> lexicographic code (A0 C1 G2 T3), per pair: std = kf ^ (kf >> 1)
+inline uint64_t kf_to_std(uint64_t x, int k) {
+    const uint64_t lo = 0x5555555555555555ull & ((k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1));
+    return x ^ ((x >> 1) & lo);
+}
+inline uint64_t std_rc(uint64_t x, int k) {
+    uint64_t r = 0;
+    for (int i = 0; i < k; ++i) {
+        r = (r << 2) | (3u - (x & 3u));
+        x >>= 2;
+    }
+    return r;
+}
+}  // namespace
+
+int kf_fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+extern "C" int kf_abi_version(void) { return KF_ABI_VERSION; }
+extern "C" const char* kf_last_error(void) { return g_err.c_str(); }
+
+extern "C" uint64_t kf_num_bins(int k) {
+    if (k < 1 || k > 15) return 0;
+    const uint64_t n = 1ull << (2 * k);
+    const uint64_t pal = (k % 2 == 0) ? (1ull << k) : 0;
+    return (n + pal) / 2;
+}
+
+// main.py:278-296 (vocab file per k) + main.py:327-328 (left merge onto it).
+extern "C" int kf_tables(int k, uint32_t* code2col, uint32_t* col2rep, uint64_t* nbins) {
+    if (k < 1 || k > KF_MAX_K) return kf_fail(KF_EINVAL, "k=%d out of range [1, %d]", k, KF_MAX_K);
+    const uint64_t n = 1ull << (2 * k);
+    // columns: canonical classes in ascending lexicographic (std code) order
+    std::vector<uint32_t> std_col(n, 0xFFFFFFFFu);
+    uint32_t next = 0;
+    for (uint64_t s = 0; s < n; ++s)
+        if (s <= std_rc(s, k)) std_col[s] = next++;
+    for (uint64_t x = 0; x < n; ++x) {
+        const uint64_t s = kf_to_std(x, k);
+        const uint64_t c = std::min(s, std_rc(s, k));
+        const uint32_t col = std_col[c];
+        if (code2col) code2col[x] = col;
+        if (col2rep && x <= kf_rc(x, k)) col2rep[col] = (uint32_t)x;   // kernel counts under min(code, rc)
+    }
+    if (nbins) *nbins = next;
+    return KF_OK;
+}
+
+extern "C" int kf_vocab_text(int k, char* out, uint64_t cap, uint64_t* written) {
+    if (k < 1 || k > KF_MAX_K) return kf_fail(KF_EINVAL, "k=%d out of range", k);
+    const uint64_t need = kf_num_bins(k) * (uint64_t)(k + 1);
+    if (written) *written = need;
+    if (!out || cap < need) return kf_fail(KF_ERANGE, "vocab buffer too small (%llu < %llu)",
+                                           (unsigned long long)cap, (unsigned long long)need);
+    static const char B[4] = {'A', 'C', 'G', 'T'};
+    const uint64_t n = 1ull << (2 * k);
+    char* p = out;
+    for (uint64_t s = 0; s < n; ++s) {
+        if (s > std_rc(s, k)) continue;
+        for (int i = k - 1; i >= 0; --i) *p++ = B[(s >> (2 * i)) & 3];
+        *p++ = '\n';
+    }
+    return KF_OK;
+}
+
+// ------------------------------------------------------------------ record index
+namespace {
+struct IvOut {
+    uint64_t* out;
+    uint64_t cap, n, base, last_e;
+    void add(uint64_t s, uint64_t e) {
+        if (e <= s) return;
+        if (n && s <= last_e + 1) {   // merge (gap of at most the one '\n' between lines)
+            last_e = std::max(last_e, e);
+            if (out && n <= cap) out[2 * (n - 1) + 1] = last_e + base;
+            return;
+        }
+        if (out && n < cap) {
+            out[2 * n] = s + base;
+            out[2 * n + 1] = e + base;
+        }
+        ++n;
+        last_e = e;
+    }
+};
+
+inline uint64_t line_end(const uint8_t* b, uint64_t i, uint64_t len) {
+    const void* p = memchr(b + i, '\n', len - i);
+    return p ? (uint64_t)((const uint8_t*)p - b) : len;
+}
+}  // namespace
+
+extern "C" int kf_index_records(const uint8_t* bytes, uint64_t len, int fmt, uint64_t base,
+                                uint64_t* out_iv, uint64_t cap_pairs, uint64_t* n_pairs, int* fmt_detected) {
+    if (!bytes && len) return kf_fail(KF_EINVAL, "null input");
+    if (fmt == KF_FMT_AUTO) fmt = (len > 0 && bytes[0] == '@') ? KF_FMT_FASTQ : KF_FMT_FASTA;
+    if (fmt != KF_FMT_FASTA && fmt != KF_FMT_FASTQ) return kf_fail(KF_EINVAL, "unknown format %d", fmt);
+    if (fmt_detected) *fmt_detected = fmt;
+    IvOut iv{out_iv, cap_pairs, 0, base, 0};
+    if (fmt == KF_FMT_FASTA) {
+        // header = a line starting with '>' (record boundary), up to its '\n'
+        uint64_t i = 0;
+        while (i < len) {
+            const void* p = memchr(bytes + i, '>', len - i);
+            if (!p) break;
+            const uint64_t j = (uint64_t)((const uint8_t*)p - bytes);
+            if (j == 0 || bytes[j - 1] == '\n') {
+                const uint64_t e = line_end(bytes, j, len);
+                iv.add(j, e);
+                i = e;
+            } else {
+                i = j + 1;   // mid-line '>' is an ordinary invalid byte (k-mer reset)
+            }
+        }
+    } else {
+        // FASTQ: '@' header, sequence lines until '+', quality lines until their
+        // length reaches the sequence length (same rules as oracle scan_fastq)
+        enum { HDR, SEQ, QUAL } st = HDR;
+        uint64_t seqlen = 0, qlen = 0, i = 0;
+        while (i < len) {
+            const uint64_t j = line_end(bytes, i, len), L = j - i;
+            if (st == HDR) {
+                iv.add(i, j);
+                if (L > 0 && bytes[i] == '@') { st = SEQ; seqlen = 0; }
+            } else if (st == SEQ) {
+                if (L > 0 && bytes[i] == '+') {
+                    iv.add(i, j);
+                    st = QUAL;
+                    qlen = 0;
+                    if (seqlen == 0) st = HDR;
+                } else {
+                    seqlen += L;
+                }
+            } else {
+                iv.add(i, j);
+                qlen += L;
+                if (qlen >= seqlen) st = HDR;
+            }
+            i = j + 1;
+        }
+    }
+    if (n_pairs) *n_pairs = iv.n;
+    if (iv.n > cap_pairs) return kf_fail(KF_ERANGE, "record index needs %llu pairs", (unsigned long long)iv.n);
+    return KF_OK;
+}
+
+// ------------------------------------------------------------------ .kf formatting
+namespace {
+// Python repr(float) (PyOS_double_to_string mode 'r'): shortest round-trip digits,
+// exponent form iff decpt <= -4 or decpt > 16, ".0" appended to integral values.
+inline char* fmt_repr(double v, char* p) {
+    if (v != v) { memcpy(p, "nan", 3); return p + 3; }
+    if (v == 0.0) { memcpy(p, "0.0", 3); return p + 3; }
+    if (v < 0) { *p++ = '-'; v = -v; }
+    if (v == __builtin_inf()) { memcpy(p, "inf", 3); return p + 3; }
+    char tmp[40];
+    auto r = std::to_chars(tmp, tmp + sizeof tmp, v, std::chars_format::scientific);
+    // tmp = d[.ddd]e(+|-)XX
+    char digs[24];
+    int nd = 0;
+    const char* q = tmp;
+    while (q < r.ptr && *q != 'e') {
+        if (*q != '.') digs[nd++] = *q;
+        ++q;
+    }
+    int e10 = 0;
+    std::from_chars(q + 1 + (q[1] == '+'), r.ptr, e10);
+    const int decpt = e10 + 1;
+    if (decpt <= -4 || decpt > 16) {
+        *p++ = digs[0];
+        if (nd > 1) {
+            *p++ = '.';
+            memcpy(p, digs + 1, nd - 1);
+            p += nd - 1;
+        }
+        *p++ = 'e';
+        *p++ = e10 < 0 ? '-' : '+';
+        int a = e10 < 0 ? -e10 : e10;
+        if (a >= 100) { *p++ = (char)('0' + a / 100); a %= 100; }
+        *p++ = (char)('0' + a / 10);
+        *p++ = (char)('0' + a % 10);
+    } else if (decpt <= 0) {
+        *p++ = '0';
+        *p++ = '.';
+        for (int i = 0; i < -decpt; ++i) *p++ = '0';
+        memcpy(p, digs, nd);
+        p += nd;
+    } else if (decpt >= nd) {
+        memcpy(p, digs, nd);
+        p += nd;
+        for (int i = nd; i < decpt; ++i) *p++ = '0';
+        *p++ = '.';
+        *p++ = '0';
+    } else {
+        memcpy(p, digs, decpt);
+        p += decpt;
+        *p++ = '.';
+        memcpy(p, digs + decpt, nd - decpt);
+        p += nd - decpt;
+    }
+    return p;
+}
+
+inline char* fmt_u64(uint64_t v, char* p) {
+    auto r = std::to_chars(p, p + 24, v);
+    return r.ptr;
+}
+
+uint64_t kf_line_cap(size_t name_len, uint64_t nbins) { return name_len + 2 + nbins * 26; }
+
+// main.py:327-357
+uint64_t format_line(const char* name, const uint32_t* c, uint64_t nb, int pseudo, int raw, char* out) {
+    char* p = out;
+    const size_t nl = strlen(name);
+    memcpy(p, name, nl);
+    p += nl;
+    *p++ = ',';
+    bool all_present = nb > 0;
+    double sum = 0.0;
+    for (uint64_t i = 0; i < nb; ++i) {
+        all_present &= c[i] > 0;
+        sum += (double)c[i];        // exact: integers < 2^53
+    }
+    if (pseudo) sum += 0.5 * (double)nb;   // exact: multiples of 0.5 < 2^53
+    for (uint64_t i = 0; i < nb; ++i) {
+        if (i) *p++ = ',';
+        if (raw && !pseudo && all_present) {
+            p = fmt_u64(c[i], p);   // int64 column (no NaN from the merge)
+        } else {
+            double v = (double)c[i] + (pseudo ? 0.5 : 0.0);
+            if (!raw) v = v / sum;
+            p = fmt_repr(v, p);
+        }
+    }
+    *p++ = '\n';
+    return (uint64_t)(p - out);
+}
+}  // namespace
+
+extern "C" int kf_format_kf(const char* name, const uint32_t* counts, uint64_t nbins, int pseudocount,
+                            int raw_cnt, char* out, uint64_t cap, uint64_t* written) {
+    if (!name || (!counts && nbins)) return kf_fail(KF_EINVAL, "null argument");
+    const uint64_t need = kf_line_cap(strlen(name), nbins);
+    if (!out || cap < need) {
+        if (written) *written = need;
+        return kf_fail(KF_ERANGE, "output buffer too small (need %llu)", (unsigned long long)need);
+    }
+    const uint64_t w = format_line(name, counts, nbins, pseudocount, raw_cnt, out);
+    if (written) *written = w;
+    return KF_OK;
+}
+
+extern "C" int kf_write_kf_files(const char* dir, const char* const* names, int32_t n, const uint32_t* counts,
+                                 uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
+    if (!dir || (!names && n) || (!counts && n)) return kf_fail(KF_EINVAL, "null argument");
+    if (n_threads < 1) n_threads = 1;
+    n_threads = std::min<int>(n_threads, std::max<int32_t>(n, 1));
+    std::atomic<int32_t> next{0};
+    std::atomic<int> err{0};
+    std::string errmsg;
+    std::mutex mu;
+    auto work = [&]() {
+        std::vector<char> buf;
+        std::string path;
+        for (;;) {
+            const int32_t i = next.fetch_add(1);
+            if (i >= n || err.load()) break;
+            buf.resize(kf_line_cap(strlen(names[i]), nbins));
+            const uint64_t w = format_line(names[i], counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt,
+                                           buf.data());
+            path.assign(dir);
+            path += "/";
+            path += names[i];
+            path += ".kf";
+            FILE* f = fopen(path.c_str(), "wb");
+            bool ok = f && fwrite(buf.data(), 1, w, f) == w;
+            if (f) ok = (fclose(f) == 0) && ok;
+            if (!ok) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!err.exchange(1)) errmsg = "cannot write " + path;
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < n_threads; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    if (err.load()) return kf_fail(KF_EINVAL, "%s", errmsg.c_str());
+    return KF_OK;
+}
+
+// ------------------------------------------------------------------ synthetic layout
+extern "C" uint64_t kf_synth_header_len(int64_t g) {
+    char tmp[32];
+    return (uint64_t)snprintf(tmp, sizeof tmp, ">syn_%lld\n", (long long)g);
+}
+
+extern "C" uint64_t kf_synth_genome_bytes(int64_t g, uint64_t seq_len, int width, uint64_t align) {
+    if (width < 1) return 0;
+    const uint64_t need = kf_synth_header_len(g) + seq_len + (seq_len + (uint64_t)width - 1) / (uint64_t)width;
+    if (align < 1) align = 1;
+    return (need + align - 1) / align * align;
+}

@@ -1,0 +1,201 @@
+"""TEST INFRASTRUCTURE ONLY -- the checker, never the product path.
+
+Python side of the oracle: a ctypes handle on the C restatement
+(oracle/kmer_oracle.c) plus restatements of the post-processing that the
+reference does in pandas after Jellyfish returns:
+
+* ``kf_line``            -- kf2vec/main.py:323-357 (dump -> merge -> pseudocount ->
+                            normalise -> ``astype(str)`` -> one ``.kf`` line);
+* ``vocab_text``         -- the sorted canonical vocab files loaded at main.py:278-296;
+* ``chunk_windows``      -- the ``get_chunks`` window plan, main.py:726-838
+                            (seqtk linearise, awk N-run collapse, seqkit length
+                            filter, ``seqkit sliding`` windows) used to pin
+                            raw-count mode against toy_example/train_tree_chunks.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import re
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "build", "libkmer_oracle.so")
+_lib = None
+
+
+def build() -> str:
+    """Compile oracle/kmer_oracle.c (make -C oracle)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _SO
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO) or os.path.getmtime(_SO) < os.path.getmtime(
+                os.path.join(_HERE, "kmer_oracle.c")):
+            build()
+        L = ctypes.CDLL(_SO)
+        u64, i32, vp = ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
+        L.oracle_nbins.restype = u64
+        L.oracle_nbins.argtypes = [i32]
+        L.oracle_rank_std.argtypes = [i32, vp]
+        L.oracle_vocab.argtypes = [i32, vp]
+        L.oracle_count.argtypes = [vp, u64, i32, i32, vp, vp, vp]
+        L.oracle_count_many.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, i32]
+        L.oracle_max_threads.restype = i32
+        L.oracle_synth_header_len.restype = u64
+        L.oracle_synth_header_len.argtypes = [ctypes.c_int64]
+        L.oracle_synth_genome.argtypes = [ctypes.c_int64, u64, u64, i32, u64, vp, u64]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def nbins(k: int) -> int:
+    return int(lib().oracle_nbins(k))
+
+
+_rank_cache: dict[int, np.ndarray] = {}
+
+
+def rank_std(k: int) -> np.ndarray:
+    if k not in _rank_cache:
+        r = np.zeros(1 << (2 * k), dtype=np.uint32)
+        assert lib().oracle_rank_std(k, _ptr(r)) == 0
+        _rank_cache[k] = r
+    return _rank_cache[k]
+
+
+def vocab_text(k: int) -> bytes:
+    buf = np.zeros(nbins(k) * (k + 1), dtype=np.uint8)
+    assert lib().oracle_vocab(k, _ptr(buf)) == 0
+    return buf.tobytes()
+
+
+def count(data: bytes | np.ndarray, k: int, fmt: int = 0) -> tuple[np.ndarray, int]:
+    """Counts of one genome in vocab (column) order, and the total."""
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    c = np.zeros(nbins(k), dtype=np.uint32)
+    t = ctypes.c_uint64(0)
+    assert lib().oracle_count(_ptr(a), a.size, k, fmt, _ptr(rank_std(k)), _ptr(c), ctypes.byref(t)) == 0
+    return c, int(t.value)
+
+
+def count_many(buf: np.ndarray, off: np.ndarray, k: int, fmt: int = 0, threads: int = 0):
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    n = off.size - 1
+    c = np.zeros((n, nbins(k)), dtype=np.uint32)
+    t = np.zeros(n, dtype=np.uint64)
+    assert lib().oracle_count_many(_ptr(buf), _ptr(off), n, k, fmt, _ptr(rank_std(k)),
+                                   _ptr(c), _ptr(t), threads) == 0
+    return c, t
+
+
+def synth_genome(g: int, seed: int, seq_len: int, width: int = 80, n_period: int = 0,
+                 size: int | None = None) -> bytes:
+    h = int(lib().oracle_synth_header_len(g))
+    need = h + seq_len + (seq_len + width - 1) // width
+    size = need if size is None else size
+    out = np.zeros(size, dtype=np.uint8)
+    assert lib().oracle_synth_genome(g, seed, seq_len, width, n_period, _ptr(out), size) == 0
+    return out.tobytes()
+
+
+# ---------------------------------------------------------------------------
+# Post-processing restatement (kf2vec/main.py:323-357)
+# ---------------------------------------------------------------------------
+def kf_values(counts: np.ndarray, pseudocount: bool = False, raw_cnt: bool = False) -> list[str]:
+    """``my_merged_counts["counts"].astype(str).to_list()`` (main.py:327-345).
+
+    dtype quirk of the reference: ``pd.merge(vocab, dump, how='left')`` keeps the
+    int64 dtype of the dump's count column when every vocab k-mer is present in
+    the dump (no NaN introduced), otherwise it becomes float64 (NaN -> fillna(0)).
+    So raw counts print as "54" when no bin is empty and "54.0" otherwise.
+    """
+    c = np.asarray(counts, dtype=np.int64)
+    is_int = bool(c.size) and bool((c > 0).all())
+    if pseudocount:                                   # main.py:332-334
+        v = c.astype(np.float64) + 0.5
+        is_int = False
+    else:
+        v = c if is_int else c.astype(np.float64)
+    if not raw_cnt:                                   # main.py:340-342
+        with np.errstate(invalid="ignore", divide="ignore"):
+            v = v / v.sum()                           # int/int -> float64 true division
+        is_int = False
+    if is_int:
+        return [str(x) for x in v.tolist()]
+    return [repr(float(x)) for x in np.asarray(v, dtype=np.float64).tolist()]
+
+
+def kf_line(name: str, counts: np.ndarray, pseudocount: bool = False, raw_cnt: bool = False) -> str:
+    """One ``<sample>.kf`` file body (main.py:350-357)."""
+    return "{},".format(name) + ",".join(kf_values(counts, pseudocount, raw_cnt)) + "\n"
+
+
+def sample_name(fname: str) -> str:
+    """main.py:275"""
+    return fname.rsplit(".f", 1)[0]
+
+
+# ---------------------------------------------------------------------------
+# get_chunks window plan (kf2vec/main.py:726-838), used to pin raw-count mode.
+# ---------------------------------------------------------------------------
+CHUNK_SZ = 10000      # main.py:100
+CHUNK_CNT_THR = 5     # main.py:101
+
+
+def fasta_records(data: bytes) -> list[tuple[str, bytes]]:
+    """seqtk seq -l 0: (header line without '>', linear sequence)."""
+    recs = []
+    name, seq = None, []
+    for line in data.split(b"\n"):
+        if line.startswith(b">"):
+            if name is not None:
+                recs.append((name, b"".join(seq)))
+            name, seq = line[1:].decode(), []
+        elif name is not None:
+            seq.append(line)
+    if name is not None:
+        recs.append((name, b"".join(seq)))
+    return recs
+
+
+_NRUN = re.compile(rb"[N|n]+")   # awk gsub(/[N|n]+/,"N") (main.py:740) -- '|' included
+
+
+def chunk_windows(fna: bytes, sample: str) -> list[tuple[str, bytes]]:
+    """(chunk sample name, window sequence) in the order get_chunks concatenates
+    them (contig order = FASTA order here; the reference uses os.listdir order of
+    the split contig files, main.py:792, so row order across contigs is unpinned)."""
+    out = []
+    for hdr, seq in fasta_records(fna):
+        seq = _NRUN.sub(b"N", seq)                     # main.py:740-742
+        seq = seq.replace(b"-", b"")                   # seqkit seq -g (remove gaps)
+        if len(seq) < CHUNK_SZ:                        # seqkit seq -m 10000 (main.py:753)
+            continue
+        cid = hdr.split()[0]
+        L = len(seq)
+        tc = math.ceil(L / CHUNK_SZ)                   # main.py:813-818
+        ov = int(math.ceil((tc * CHUNK_SZ - L) / (tc - 1))) if tc != 1 else 0
+        step = CHUNK_SZ - ov
+        s = 0
+        while s + CHUNK_SZ <= L:                       # seqkit sliding (non-greedy)
+            w = "{}_sliding:{}-{}".format(cid, s + 1, s + CHUNK_SZ)
+            name = "{}.part_{}.part_{}".format(sample, cid, w).replace("sliding:", "sliding__")
+            out.append((name, seq[s:s + CHUNK_SZ]))
+            s += step
+    return out

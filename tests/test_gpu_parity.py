@@ -1,0 +1,198 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and the
+reference's golden `.kf` files.  Integer counts must be bit-exact; `.kf` bytes
+byte-exact.  Run on an MI355X: `pytest -m gpu`."""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+import gen
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev(native):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests need an MI355X")
+    return torch.device("cuda:0")
+
+
+_counters = {}
+
+
+def counter(k, dev):
+    from kf2vecfsw_amd.counter import KmerCounter
+    if k not in _counters:
+        _counters[k] = KmerCounter(k, dev)
+    return _counters[k]
+
+
+def run_batch(blobs, k, dev, offsets=None, fmt=0):
+    """Count blobs on the GPU; optional explicit (unaligned) genome offsets."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    if offsets is None:
+        hb = C.pack_genomes(blobs, fmt=fmt)
+    else:
+        total = int(offsets[-1])
+        data = torch.full((max(total, 16),), 10, dtype=torch.uint8)
+        d = data.numpy()
+        ex = []
+        for i, b in enumerate(blobs):
+            lo = int(offsets[i])
+            d[lo: lo + len(b)] = np.frombuffer(b, np.uint8)
+            iv, _ = C.index_records(d[lo: lo + len(b)], fmt, lo)
+            ex.append(iv)
+        hb = C.HostBatch(data, np.asarray(offsets, np.uint64),
+                         np.concatenate(ex).astype(np.uint64) if ex else np.zeros(0, np.uint64),
+                         [str(i) for i in range(len(blobs))])
+    db = C.to_device(hb, dev)
+    cnt, tot = counter(k, dev).count(db)
+    torch.cuda.synchronize()
+    return C.counts_to_numpy(cnt), tot.cpu().numpy()
+
+
+def check_against_oracle(oracle, blobs, k, counts, totals, fmt=0, tag=""):
+    for i, b in enumerate(blobs):
+        c, t = oracle.count(b, k, fmt)
+        assert int(totals[i]) == t, (tag, i, int(totals[i]), t)
+        if not (counts[i] == c).all():
+            bad = np.nonzero(counts[i] != c)[0][:5]
+            pytest.fail(f"{tag} genome {i} k={k}: {len(np.nonzero(counts[i] != c)[0])} bins differ, "
+                        f"e.g. cols {bad.tolist()} got {counts[i][bad].tolist()} want {c[bad].tolist()}")
+
+
+def test_toy_byte_exact(torch_dev, oracle, toy):
+    """All 7 pinned toy genomes in one batch -> `.kf` bytes equal the reference's."""
+    from kf2vecfsw_amd.main import format_kf
+    blobs = [t[2] for t in toy]
+    counts, totals = run_batch(blobs, 7, torch_dev)
+    check_against_oracle(oracle, blobs, 7, counts, totals, tag="toy")
+    for i, (name, sample, data, exp) in enumerate(toy):
+        assert format_kf(sample, counts[i]) == exp, name
+
+
+@pytest.mark.parametrize("k", list(range(2, 13)))
+def test_random_fasta_all_k(torch_dev, oracle, k):
+    rng = np.random.default_rng(100 + k)
+    blobs = [gen.random_fasta(rng, int(rng.integers(0, 40000)), max_records=6, n_rate=0.002,
+                              iupac_rate=0.0005, lower=0.05, crlf_rate=0.1, poly_rate=0.01)
+             for _ in range(24)]
+    blobs += [b"", b">only header\n", b"ACGT", b"\n\n\n", b">x\n" + b"A" * 5000 + b"\n"]
+    counts, totals = run_batch(blobs, k, torch_dev)
+    check_against_oracle(oracle, blobs, k, counts, totals, tag="rand")
+
+
+@pytest.mark.parametrize("k", [3, 7, 8, 11])
+def test_unaligned_genome_offsets(torch_dev, oracle, k):
+    """Genome boundaries at arbitrary byte offsets (not 16-aligned) and genomes
+    smaller than one lane block / one chunk."""
+    rng = np.random.default_rng(7 * k)
+    sizes = [0, 1, 5, 15, 16, 17, 33, 1023, 1024, 1025, 3000, 70000]
+    blobs = []
+    for s in sizes * 3:
+        b = gen.random_fasta(rng, s, max_records=3, n_rate=0.001)
+        blobs.append(b)
+    rng.shuffle(blobs)
+    gaps = rng.integers(0, 40, size=len(blobs))
+    off = [0]
+    for b, g in zip(blobs, gaps):
+        off.append(off[-1] + len(b) + int(g))
+    counts, totals = run_batch(blobs, k, torch_dev, offsets=off)
+    check_against_oracle(oracle, blobs, k, counts, totals, tag="unaligned")
+
+
+@pytest.mark.parametrize("width", [1, 2, 3, 5, 6, 7, 10, 16, 60, 80])
+def test_short_lines_and_blank_lines(torch_dev, oracle, width):
+    """Very short lines exercise the slow context scan (lanes with < k-1 bases)."""
+    rng = np.random.default_rng(width)
+    blobs = []
+    for _ in range(6):
+        seq = gen.random_seq(rng, int(rng.integers(1000, 30000)), n_rate=0.001)
+        body = gen.wrap(seq, width)
+        if rng.random() < 0.5:
+            body = body.replace(b"\n", b"\n\n", 7)
+        blobs.append(b">r\n" + body)
+    blobs.append(b">e\n" + b"\n" * 5000 + b"ACGTACGTACGTTT\n" + b"\n" * 3000 + b"GGGCCC\n")
+    for k in (3, 7, 9):
+        counts, totals = run_batch(blobs, k, torch_dev)
+        check_against_oracle(oracle, blobs, k, counts, totals, tag=f"w{width}")
+
+
+def test_fastq(torch_dev, oracle):
+    rng = np.random.default_rng(5)
+    blobs = [gen.random_fastq(rng, int(rng.integers(0, 400)), n_rate=0.01, multiline=bool(i % 2))
+             for i in range(10)]
+    for k in (5, 7, 10):
+        counts, totals = run_batch(blobs, k, torch_dev)
+        check_against_oracle(oracle, blobs, k, counts, totals, tag="fastq")
+
+
+def test_one_large_genome_split_across_all_workgroups(torch_dev, oracle):
+    """One 60 MB genome: every workgroup / wave boundary needs exact warm-up context."""
+    rng = np.random.default_rng(9)
+    seq = gen.random_seq(rng, 60_000_000, n_rate=1e-5, lower=0.01)
+    blob = b">big\n" + gen.wrap(seq, 61)
+    for k in (7, 9):
+        counts, totals = run_batch([blob], k, torch_dev)
+        check_against_oracle(oracle, [blob], k, counts, totals, tag="big")
+
+
+def test_many_small_genomes(torch_dev, oracle):
+    """10k chunk-sized genomes (get_chunks style windows): many genome pieces per workgroup."""
+    rng = np.random.default_rng(10)
+    blobs = [b">w\n" + gen.wrap(gen.random_seq(rng, int(rng.integers(50, 12000))), 80) for _ in range(10000)]
+    counts, totals = run_batch(blobs, 7, torch_dev)
+    check_against_oracle(oracle, blobs, 7, counts, totals, tag="small")
+
+
+def test_device_synth_matches_oracle_and_counts(torch_dev, oracle):
+    from kf2vecfsw_amd import counter as C
+    import torch
+    n, L = 5, 300_000
+    for n_period in (0, 3):
+        db = C.synth_device_batch(n, L, seed0=20260101, width=80, n_period=n_period, g0=11, device=torch_dev)
+        cnt, tot = counter(7, torch_dev).count(db)
+        torch.cuda.synchronize()
+        host = db.data.cpu().numpy()
+        off = db.off.cpu().numpy()
+        counts = C.counts_to_numpy(cnt)
+        for i in range(n):
+            exp = oracle.synth_genome(11 + i, 20260101 + 11 + i, L, 80, n_period, int(off[i + 1] - off[i]))
+            assert host[off[i]: off[i + 1]].tobytes() == exp
+            c, t = oracle.count(exp, 7)
+            assert int(tot[i]) == t and (counts[i] == c).all()
+            if n_period == 0:
+                assert t == L - 7 + 1
+
+
+def test_deterministic_and_accumulate(torch_dev, oracle):
+    import torch
+    from kf2vecfsw_amd import counter as C
+    db = C.synth_device_batch(16, 1_000_000, seed0=1, device=torch_dev)
+    kc = counter(7, torch_dev)
+    a, ta = kc.count(db)
+    a = a.clone()
+    b, tb = kc.count(db)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(ta, tb)
+    kc.count(db, b, tb, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(b, 2 * a) and torch.equal(tb, 2 * ta)
+
+
+def test_cli_end_to_end_toy(torch_dev, toy, tmp_path):
+    """`get_frequencies` CLI mirror on the toy genomes == committed `.kf` bytes."""
+    from kf2vecfsw_amd import main as M
+    inp, out = tmp_path / "in", tmp_path / "out"
+    inp.mkdir()
+    out.mkdir()
+    for name, sample, data, exp in toy:
+        (inp / name).write_bytes(data)
+    M.main(["get_frequencies", "-input_dir", str(inp), "-output_dir", str(out), "-k", "7", "-p", "4"])
+    for name, sample, data, exp in toy:
+        assert (out / (sample + ".kf")).read_bytes() == exp, sample
+    assert sorted(os.listdir(out)) == sorted(t[1] + ".kf" for t in toy)

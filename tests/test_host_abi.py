@@ -1,0 +1,137 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol of
+include/kf2vec_gpu.h, and its host half (bin tables, vocab, record index,
+`.kf` formatter/writer) matches the oracle.  No device calls."""
+import ctypes
+import gzip
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, TOY
+import gen
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "kf2vec_gpu.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(kf_\w+)\s*\(", txt, re.M)))
+
+
+def test_exports_every_header_symbol(native):
+    from kf2vecfsw_amd import _native
+    syms = header_symbols()
+    assert len(syms) >= 13
+    for s in syms:
+        assert hasattr(native, s), s
+    assert set(syms) == set(_native.SIGNATURES), "ctypes signatures out of sync with the header"
+    assert native.kf_abi_version() == 1
+
+
+def test_tables_match_oracle(native, oracle):
+    from kf2vecfsw_amd import counter as C
+    for k in range(2, 12):
+        c2c, c2r = C.tables(k)
+        x = np.arange(1 << (2 * k), dtype=np.uint64)
+        s = x ^ ((x >> np.uint64(1)) & np.uint64(int("01" * k, 2)))   # kf code -> lexicographic code
+        assert (c2c == oracle.rank_std(k)[s]).all(), k
+        nb = C.num_bins(k)
+        assert nb == oracle.nbins(k)
+        assert (c2c[c2r] == np.arange(nb)).all()
+        # the representative is min(code, revcomp(code)) in kf code
+        rc = np.zeros_like(x)
+        y = x.copy()
+        for _ in range(k):
+            rc = (rc << np.uint64(2)) | ((y & np.uint64(3)) ^ np.uint64(2))
+            y >>= np.uint64(2)
+        assert (c2r == np.minimum(x, rc)[c2r]).all()
+
+
+def test_vocab_text_matches_oracle(native, oracle):
+    from kf2vecfsw_amd import counter as C
+    for k in range(3, 12):
+        assert C.vocab_text(k) == oracle.vocab_text(k)
+
+
+def test_format_kf_matches_reference_goldens(native, oracle):
+    from kf2vecfsw_amd.main import format_kf
+    for fd, kd in [("train_tree_fna", "train_tree_kf"), ("test_fna", "test_kf")]:
+        for f in sorted(os.listdir(os.path.join(TOY, fd))):
+            sample = f[:-3].rsplit(".f", 1)[0]
+            c, _ = oracle.count(gzip.open(os.path.join(TOY, fd, f)).read(), 7)
+            exp = gzip.open(os.path.join(TOY, kd, sample + ".kf.gz")).read()
+            assert format_kf(sample, c) == exp
+
+
+@pytest.mark.parametrize("pseudo", [False, True])
+@pytest.mark.parametrize("raw", [False, True])
+def test_format_kf_modes_match_oracle(native, oracle, pseudo, raw):
+    from kf2vecfsw_amd.main import format_kf
+    rng = np.random.default_rng(7)
+    cases = [rng.integers(0, 2 ** 32 - 1, size=4000, dtype=np.uint64).astype(np.uint32),
+             rng.integers(0, 3, size=8192).astype(np.uint32),
+             rng.integers(1, 100, size=2080).astype(np.uint32),          # all bins present -> int dtype
+             np.zeros(32, np.uint32), np.ones(1, np.uint32),
+             (rng.pareto(1.0, size=8192) * 10).astype(np.uint32)]
+    for c in cases:
+        assert format_kf("s", c, pseudo, raw).decode() == oracle.kf_line("s", c, pseudo, raw)
+
+
+def test_write_kf_files(native, oracle, tmp_path):
+    from kf2vecfsw_amd.main import write_kf_files
+    rng = np.random.default_rng(3)
+    c = rng.integers(0, 50, size=(9, 512)).astype(np.uint32)
+    names = ["g%d" % i for i in range(9)]
+    write_kf_files(str(tmp_path), names, c, False, False, 4)
+    for i, n in enumerate(names):
+        assert (tmp_path / (n + ".kf")).read_text() == oracle.kf_line(n, c[i])
+
+
+def test_index_records_fasta_semantics(native, oracle):
+    """Index + device semantics (newline-transparent, excluded = reset) count
+    exactly what the oracle's own FASTA parser counts."""
+    from kf2vecfsw_amd import counter as C
+    rng = np.random.default_rng(11)
+    for t in range(40):
+        data = gen.random_fasta(rng, int(rng.integers(0, 3000)), n_rate=0.01, iupac_rate=0.002, lower=0.1,
+                                crlf_rate=0.2)
+        base = int(rng.integers(0, 1 << 40))
+        iv, fmt = C.index_records(np.frombuffer(data, np.uint8), 0, base)
+        assert fmt == 1 and (np.diff(iv.astype(np.int64)) > 0).all() if iv.size else True
+        k = int(rng.integers(2, 9))
+        got = gen.model_count(data, iv, base, k, oracle.rank_std(k))
+        exp = oracle.count(data, k, 1)
+        assert got[1] == exp[1] and (got[0] == exp[0]).all(), t
+
+
+def test_index_records_fastq_semantics(native, oracle):
+    from kf2vecfsw_amd import counter as C
+    rng = np.random.default_rng(12)
+    for t in range(20):
+        data = gen.random_fastq(rng, int(rng.integers(0, 30)), n_rate=0.01, multiline=bool(t % 2))
+        iv, fmt = C.index_records(np.frombuffer(data, np.uint8), 0, 0)
+        if data:
+            assert fmt == 2
+        k = int(rng.integers(2, 9))
+        got = gen.model_count(data, iv, 0, k, oracle.rank_std(k))
+        exp = oracle.count(data, k, 0)
+        assert got[1] == exp[1] and (got[0] == exp[0]).all(), t
+
+
+def test_index_records_range_error(native):
+    from kf2vecfsw_amd import _native as N
+    data = b">a\nAC\n>b\nGT\n>c\nTT\n"
+    out = np.zeros(2, np.uint64)
+    n = ctypes.c_uint64(0)
+    rc = N.lib().kf_index_records(data, len(data), 0, 0, out.ctypes.data, 1, ctypes.byref(n), None)
+    assert rc == N.KF_ERANGE and n.value == 3
+    assert N.lib().kf_last_error().decode().startswith("record index needs")
+
+
+def test_count_batch_rejects_bad_args(native):
+    from kf2vecfsw_amd import _native as N
+    L = N.lib()
+    assert L.kf_count_batch(None, None, 1, None, 0, None, None, 7, None, None, 0, None) == N.KF_EINVAL
+    assert L.kf_count_batch(None, None, 1, None, 0, None, None, 13, None, None, 0, None) == N.KF_EINVAL
+    assert b"k out of range" in L.kf_last_error()
+    assert L.kf_count_batch(None, None, 0, None, 0, None, None, 7, None, None, 0, None) == N.KF_OK

@@ -1,0 +1,85 @@
+"""Pins the CPU oracle (oracle/) against every golden vector the reference holds
+for this path: the 7 toy `.kf` files with their `.fna` (get_frequencies,
+normalised), the 3 chunk `.kf` files (get_chunks -> get_frequencies -raw_cnt,
+kf2vec/main.py:869-881) and the vocab files (main.py:278-296)."""
+import gzip
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, TOY
+
+
+def test_oracle_toy_kf_byte_exact(oracle, toy):
+    assert len(toy) == 7
+    for name, sample, data, exp in toy:
+        c, total = oracle.count(data, 7)
+        assert int(c.sum()) == total
+        assert oracle.kf_line(sample, c).encode() == exp, name
+
+
+@pytest.mark.parametrize("sample", ["G000830275", "G000830295", "G000402355"])
+def test_oracle_chunks_raw_byte_exact(oracle, sample):
+    fna = gzip.open(os.path.join(TOY, "train_tree_fna", sample + ".fna.gz")).read()
+    exp = gzip.open(os.path.join(TOY, "train_tree_chunks", sample + ".kf.gz")).read().decode()
+    rows = exp.splitlines(keepends=True)
+    got = {}
+    for name, seq in oracle.chunk_windows(fna, sample):
+        c, _ = oracle.count(b">w\n" + seq + b"\n", 7)
+        got[name] = oracle.kf_line(name, c, raw_cnt=True)
+    assert len(got) == len(rows)
+    for r in rows:
+        assert got[r.split(",", 1)[0]] == r
+
+
+def test_oracle_vocab_matches_reference_files(oracle):
+    ref = json.load(open(os.path.join(GOLDEN, "vocab_sha256.json")))["vocab"]
+    for k, (n, sha, _) in ref.items():
+        t = oracle.vocab_text(int(k))
+        assert t.count(b"\n") == n == oracle.nbins(int(k))
+        assert hashlib.sha256(t).hexdigest() == sha
+
+
+def test_oracle_small_cases(oracle):
+    # hand-checked: ACGT has k=2 mers AC, CG, GT -> canonical AC, CG, AC
+    c, t = oracle.count(b">x\nACGT\n", 2)
+    vocab = oracle.vocab_text(2).split()
+    got = {vocab[i].decode(): int(v) for i, v in enumerate(c) if v}
+    assert got == {"AC": 2, "CG": 1} and t == 3
+    # line breaks are transparent, records and N break k-mers
+    a, _ = oracle.count(b">x\nAC\nGT\n", 2)
+    assert (a == c).all()
+    b, tb = oracle.count(b">x\nAC\n>y\nGT\n", 2)
+    assert tb == 2
+    n, tn = oracle.count(b">x\nACNGT\n", 2)
+    assert tn == 2
+    low, _ = oracle.count(b">x\nacgt\n", 2)
+    assert (low == c).all()
+    # FASTQ: only sequence lines count, quality may contain ACGT
+    fq, tq = oracle.count(b"@r1\nACGT\n+\nACGT\n@r2\nAC\nGT\n+\nII\nII\n", 2)
+    assert tq == 3 + 3
+    # empty genome
+    z, tz = oracle.count(b"", 7)
+    assert tz == 0 and not z.any()
+
+
+def test_kf_values_quirks(oracle):
+    c = np.array([3, 0, 1], dtype=np.uint32)
+    assert oracle.kf_values(c, raw_cnt=True) == ["3.0", "0.0", "1.0"]
+    assert oracle.kf_values(np.array([3, 2, 1]), raw_cnt=True) == ["3", "2", "1"]
+    assert oracle.kf_values(np.array([3, 2, 1]), pseudocount=True, raw_cnt=True) == ["3.5", "2.5", "1.5"]
+    assert oracle.kf_values(np.array([1, 1, 2])) == ["0.25", "0.25", "0.5"]
+    assert oracle.kf_values(np.zeros(2)) == ["nan", "nan"]
+
+
+def test_oracle_synth_spec(oracle):
+    g = oracle.synth_genome(3, 20260101 + 3, 1000, 80)
+    assert g.startswith(b">syn_3\n")
+    lines = g.split(b"\n")
+    assert all(len(x) == 80 for x in lines[1:-2]) and len(lines[-2]) == 40
+    assert set(b"".join(lines[1:])) <= set(b"ACGT")
+    gn = oracle.synth_genome(3, 7, 300000, 80, n_period=2)
+    assert b"N" in gn
