@@ -87,7 +87,8 @@ int kf_index_records(const uint8_t* bytes, uint64_t len, int fmt, uint64_t base,
 /* Count canonical k-mers of a batch of genomes already resident in HBM
  * (replaces `jellyfish count -C` + `jellyfish dump -c`, main.py:309-323).
  *   d_bytes    : batch bytes, 16-byte aligned; genome g is
- *                d_bytes[d_goff[g], d_goff[g+1])
+ *                d_bytes[d_goff[g], d_goff[g+1]); the allocation must be readable
+ *                up to d_goff[n] rounded up to 16 bytes (vector loads)
  *   d_goff     : n_genomes+1 non-decreasing offsets (device)
  *   d_excl     : 2*n_excl sorted disjoint [start,end) pairs (device) from
  *                kf_index_records, positions absolute in d_bytes (may be NULL if 0)

@@ -59,6 +59,11 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise NativeError(f"{LIB_PATH} not found: build it with `python -m kf2vecfsw_amd.build`")
+        # PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7).  Load it
+        # first so our NEEDED libamdhip64.so.7 binds to the SAME HIP runtime instance;
+        # otherwise the process holds two runtimes and torch's stream handles and
+        # device pointers are invalid in ours (hipMemsetAsync fails).
+        import torch  # noqa: F401
         try:
             L = ctypes.CDLL(LIB_PATH)
         except OSError as e:  # pragma: no cover - environment specific

@@ -195,8 +195,13 @@ __device__ __forceinline__ void apply_masks(const CountArgs& A, uint64_t chunk, 
     }
 }
 
+// Buffer descriptor of the chunk at c, clamped to the genome end rounded up to
+// 16 bytes: the hardware range check zeroes a whole dword/vector that straddles
+// num_records, so an exact (unaligned) end would drop the genome's last bases.
+// Bytes in [ghi, align16(ghi)) are read but never counted (they lie past hi).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const uint8_t* bytes, uint64_t c, uint64_t ghi) {
-    const uint32_t rec = c >= ghi ? 0u : (uint32_t)min<uint64_t>(ghi - c, (uint64_t)kChunk);
+    const uint64_t end = (ghi + 15) & ~(uint64_t)15;
+    const uint32_t rec = c >= end ? 0u : (uint32_t)min<uint64_t>(end - c, (uint64_t)kChunk);
     return __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c), (short)0, (int)rec, 0x00020000);
 }
 

@@ -38,7 +38,7 @@ def run_batch(blobs, k, dev, offsets=None, fmt=0):
         hb = C.pack_genomes(blobs, fmt=fmt)
     else:
         total = int(offsets[-1])
-        data = torch.full((max(total, 16),), 10, dtype=torch.uint8)
+        data = torch.full((max((total + 15) // 16 * 16, 16),), 10, dtype=torch.uint8)
         d = data.numpy()
         ex = []
         for i, b in enumerate(blobs):
@@ -196,3 +196,17 @@ def test_cli_end_to_end_toy(torch_dev, toy, tmp_path):
     for name, sample, data, exp in toy:
         assert (out / (sample + ".kf")).read_bytes() == exp, sample
     assert sorted(os.listdir(out)) == sorted(t[1] + ".kf" for t in toy)
+
+
+def test_genome_end_at_every_alignment(torch_dev, oracle):
+    """Unterminated genomes ending at every byte offset mod 16, packed with no gap:
+    the last bases sit in a vector load that straddles the genome end."""
+    rng = np.random.default_rng(77)
+    blobs = [b">x\n" + gen.random_seq(rng, 100 + r + 16 * int(rng.integers(0, 70))).tobytes() for r in range(16)]
+    blobs += [b">y\n" + gen.random_seq(rng, 1008 + r).tobytes() for r in range(16)]
+    off = [0]
+    for b in blobs:
+        off.append(off[-1] + len(b))
+    for k in (3, 7, 11):
+        counts, totals = run_batch(blobs, k, torch_dev, offsets=off)
+        check_against_oracle(oracle, blobs, k, counts, totals, tag="end-align")
