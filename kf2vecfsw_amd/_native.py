@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkf2vec_gpu.so")
+# KF2VEC_GPU_LIB may point at a profiling build (e.g. libkf2vec_gpu_ablation.so)
+LIB_PATH = os.environ.get("KF2VEC_GPU_LIB") or os.path.join(_HERE, "libkf2vec_gpu.so")
 
 KF_OK = 0
 KF_EINVAL = -1

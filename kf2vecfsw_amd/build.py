@@ -29,15 +29,17 @@ def _stale() -> bool:
     return any(os.path.getmtime(os.path.join(CSRC, d)) > t for d in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, ablation: bool = False, out: str | None = None) -> str:
+    """ablation=True adds profiling-only kernel variants (KF_COUNT_VARIANT 2, 3)."""
+    out = out or OUT
+    if not force and not ablation and out == OUT and not _stale():
         return OUT
     os.makedirs(BUILD, exist_ok=True)
     objs = []
     for s in SOURCES_HIP:
         o = os.path.join(BUILD, s + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-c", os.path.join(CSRC, s), "-o", o]
+               "-c", os.path.join(CSRC, s), "-o", o] + (["-DKF_ABLATION"] if ablation else [])
         if verbose:
             cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
         subprocess.run(cmd, check=True)
@@ -47,12 +49,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
         subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-pthread",
                         "-c", os.path.join(CSRC, s), "-o", o], check=True)
         objs.append(o)
-    tmp = OUT + ".tmp"
+    tmp = out + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs, "-o", tmp],
                    check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))
+    abl = "--ablation" in sys.argv
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, ablation=abl,
+                out=os.path.join(HERE, "libkf2vec_gpu_ablation.so") if abl else None))

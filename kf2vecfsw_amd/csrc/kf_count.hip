@@ -23,6 +23,7 @@
 // (kf_index_records) and are treated as invalid bytes (k-mer reset).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kf_internal.h"
 
@@ -30,8 +31,24 @@ namespace kf {
 
 constexpr int kWave = 64;
 constexpr int kChunk = 1024;       // bytes per wave iteration (64 lanes x 16 B)
-constexpr int kBlock = 512;        // threads per workgroup
-constexpr int kWaves = kBlock / kWave;
+// Workgroup shapes ("variants"): one 4^k-entry LDS histogram is shared by all
+// waves of a workgroup, so a bigger workgroup raises occupancy at equal LDS.
+//   variant 0: 512 threads (8 waves), 2 workgroups/CU at k=7
+//   variant 1: 1024 threads (16 waves), 8 waves/SIMD register budget
+#ifdef KF_ABLATION
+constexpr int kNumVariants = 4;
+#else
+constexpr int kNumVariants = 2;
+#endif
+constexpr int kDefaultVariant = 1;
+template <int V> struct Shape;
+template <> struct Shape<0> { static constexpr int block = 512, wpe = 0, abl = 0; };
+template <> struct Shape<1> { static constexpr int block = 1024, wpe = 8, abl = 0; };
+#ifdef KF_ABLATION
+// profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
+template <> struct Shape<2> { static constexpr int block = 1024, wpe = 8, abl = 1; };   // no LDS adds
+template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 3; };   // stream bytes only
+#endif
 constexpr int kLdsMaxK = 7;        // 4^7 x 4 B = 64 KiB histogram
 
 struct CountArgs {
@@ -83,7 +100,7 @@ __device__ __forceinline__ bool tail_complete(uint32_t t) {
 __device__ __forceinline__ void classify16(const uint4 d, uint32_t& C, uint32_t& INV, uint32_t& NL) {
     const uint32_t w[4] = {d.x, d.y, d.z, d.w};
     uint32_t pc[4];
-    int pv[4], pn[4];
+    int pv[4], pn[4];   // flag nibbles
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t x = w[q];
@@ -93,33 +110,47 @@ __device__ __forceinline__ void classify16(const uint4 d, uint32_t& C, uint32_t&
         const uint32_t vf = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, y);
         const uint32_t nf = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, x ^ 0x06060606u);
         pc[q] = __builtin_amdgcn_udot4(cb, 0x01041040u, 0u, false);
-        pv[q] = __builtin_amdgcn_sdot4((int)vf, 0x01020408, 0, false);
-        pn[q] = __builtin_amdgcn_sdot4((int)nf, 0x01020408, 0, false);
+        // flag bytes are 0x00 / 0xFF (= -1 signed); weights -8,-4,-2,-1 give the
+        // positive nibble directly (no negation, no multiply in the combine)
+        pv[q] = __builtin_amdgcn_sdot4((int)vf, (int)0xFFFEFCF8u, 0, false);
+        pn[q] = __builtin_amdgcn_sdot4((int)nf, (int)0xFFFEFCF8u, 0, false);
     }
     C = (pc[0] << 24) | (pc[1] << 16) | (pc[2] << 8) | pc[3];
-    // pv/pn are minus the flag nibbles; sum them modulo 2^32 and negate once
-    INV = 0u - (((uint32_t)pv[0] << 12) + ((uint32_t)pv[1] << 8) + ((uint32_t)pv[2] << 4) + (uint32_t)pv[3]);
-    NL = 0xFFFFu & ~(0u - (((uint32_t)pn[0] << 12) + ((uint32_t)pn[1] << 8) + ((uint32_t)pn[2] << 4) +
-                           (uint32_t)pn[3]));
+    INV = ((uint32_t)pv[0] << 12) | ((uint32_t)pv[1] << 8) | ((uint32_t)pv[2] << 4) | (uint32_t)pv[3];
+    NL = 0xFFFFu ^ (((uint32_t)pn[0] << 12) | ((uint32_t)pn[1] << 8) | ((uint32_t)pn[2] << 4) | (uint32_t)pn[3]);
 }
 
-// Remove newline entries (compaction).  C: 2-bit entries, V/EN: 1-bit masks.
+// Remove newline entries (compaction).  C: 2-bit entries, V/EN: 1-bit masks,
+// entry r at bits [2r, 2r+2) / bit r.  The lowest newline is removed branch-free
+// (r = 16 sentinel when there is none: every mask becomes the identity); any
+// further newline in the same 16 bytes (lines shorter than 16) takes the loop.
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+template <bool MASKED>
+__device__ __forceinline__ void remove_entry(uint32_t r, uint32_t& C, uint32_t& V, uint32_t& EN, uint32_t& nl) {
+    const uint32_t lo1 = (1u << r) - 1u;          // entries below r stay
+    const uint32_t lo2 = lo1 | (lo1 << r);         // (1 << 2r) - 1, also for r = 16
+    V = bfi(lo1, V, V >> 1);
+    if (MASKED) EN = bfi(lo1, EN, EN >> 1);
+    C = bfi(lo2, C, C >> 2);
+    nl = (nl >> 1) & ~lo1;                         // drop bit r, shift the rest down
+}
+
 template <bool MASKED>
 __device__ __forceinline__ void compact(uint32_t nl, uint32_t& C, uint32_t& V, uint32_t& EN) {
-    while (nl) {
-        const uint32_t r = __builtin_ctz(nl);
-        const uint32_t lo1 = (1u << r) - 1u;
-        V = ((V >> (r + 1)) << r) | (V & lo1);
-        if (MASKED) EN = ((EN >> (r + 1)) << r) | (EN & lo1);
-        const uint32_t lo2 = (1u << (2 * r)) - 1u;
-        C = (((C >> (2 * r + 1)) >> 1) << (2 * r)) | (C & lo2);
-        nl = (nl >> (r + 1)) << r;
-    }
+    remove_entry<MASKED>((uint32_t)__builtin_ctz(nl | 0x10000u), C, V, EN, nl);
+    while (nl) remove_entry<MASKED>((uint32_t)__builtin_ctz(nl), C, V, EN, nl);
 }
 
 __device__ __forceinline__ uint32_t revpairs(uint32_t x) {
     const uint32_t t = __builtin_bitreverse32(x);
     return ((t << 1) & 0xAAAAAAAAu) | ((t >> 1) & 0x55555555u);
+}
+
+// reverse complement of a K-mer in kf code (complement = code ^ 2)
+template <int K>
+__device__ __forceinline__ uint32_t kf_revcomp(uint32_t x) {
+    return (revpairs(x) >> (32 - 2 * K)) ^ (0xAAAAAAAAu >> (32 - 2 * K));
 }
 
 template <int K>
@@ -261,7 +292,7 @@ __device__ __noinline__ uint32_t chunk_tail(const uint8_t* bytes, const uint64_t
 }
 
 // Count one chunk.  GLOBAL = count straight into d_counts (k > kLdsMaxK).
-template <int K, bool MASKED, bool GLOBAL>
+template <int K, bool MASKED, bool GLOBAL, int ABL>
 __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
                                                 const ChunkMask& m, uint64_t iv0, uint32_t carry,
                                                 uint32_t* __restrict__ hist, uint32_t* __restrict__ gcounts,
@@ -283,30 +314,46 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
     if (MASKED) R &= EN;
 
     const uint32_t wlo = (uint32_t)W, whi = (uint32_t)(W >> 32);
-    const uint32_t rhi = revpairs(wlo) ^ 0xAAAAAAAAu;   // revcomp of the 64-bit window
-    const uint32_t rlo = revpairs(whi) ^ 0xAAAAAAAAu;
-    constexpr int RS = 2 * (17 - K);
-    const uint32_t rplo = __builtin_amdgcn_alignbit(rhi, rlo, RS);
-    const uint32_t rphi = rhi >> RS;
     const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
                             __builtin_amdgcn_alignbit(whi, wlo, 24)};
-    const uint32_t rv[4] = {rplo, __builtin_amdgcn_alignbit(rphi, rplo, 8),
-                            __builtin_amdgcn_alignbit(rphi, rplo, 16), __builtin_amdgcn_alignbit(rphi, rplo, 24)};
+    // forward window ending at entry r: bits [2r, 2r+2K) of W (first base highest)
+    auto fwd = [&](int r) -> uint32_t {
+        const int fo = (2 * r) & ~7;
+        return __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, W2);
+    };
     if (!GLOBAL) {
+        // LDS path: count FORWARD k-mers only into the 4^k histogram; a k-mer and
+        // its reverse complement are merged into one canonical bin at flush time.
+        // Fast case (uniform): every window valid except possibly the 16th (a
+        // newline in the block leaves 15 entries) -> no per-window inc extraction.
+        const bool fast = !MASKED && __ballot((R | 0x8000u) != 0xFFFFu) == 0;
+        if (ABL == 0 && fast) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int fo = (2 * r) & ~7;
-            const uint32_t f = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, W2);
-            const int rr = 2 * (15 - r), ro = rr & ~7;
-            const uint32_t c = __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, W2);
-            const uint32_t inc = (R >> r) & 1u;
-            __hip_atomic_fetch_add(hist + min(f, c), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            for (int r = 0; r < 15; ++r)
+                __hip_atomic_fetch_add(hist + fwd(r), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(hist + fwd(15), R >> 15, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t inc = (R >> r) & 1u;
+                if (ABL == 0)
+                    __hip_atomic_fetch_add(hist + fwd(r), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else   // profiling only (no LDS traffic)
+                    lane_total += fwd(r) ^ inc;
+            }
         }
     } else {
+        // global path: canonical = min(fwd, revcomp) in kf code, then column via code2col
+        const uint32_t rhi = revpairs(wlo) ^ 0xAAAAAAAAu;   // revcomp of the 64-bit window
+        const uint32_t rlo = revpairs(whi) ^ 0xAAAAAAAAu;
+        constexpr int RS = 2 * (17 - K);
+        const uint32_t rplo = __builtin_amdgcn_alignbit(rhi, rlo, RS);
+        const uint32_t rphi = rhi >> RS;
+        const uint32_t rv[4] = {rplo, __builtin_amdgcn_alignbit(rphi, rplo, 8),
+                                __builtin_amdgcn_alignbit(rphi, rplo, 16), __builtin_amdgcn_alignbit(rphi, rplo, 24)};
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int fo = (2 * r) & ~7;
-            const uint32_t f = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, W2);
+            const uint32_t f = fwd(r);
             const int rr = 2 * (15 - r), ro = rr & ~7;
             const uint32_t c = __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, W2);
             if ((R >> r) & 1u) {
@@ -322,7 +369,7 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
 }
 
 // Process the wave range [lo, hi) of genome [glo, ghi).
-template <int K, bool GLOBAL>
+template <int K, bool GLOBAL, int ABL>
 __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                   uint64_t lo, uint64_t hi, int lane,
                                                   uint32_t* __restrict__ hist) {
@@ -372,10 +419,12 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
         }
         const bool has_iv = iv_s < c + kChunk;
         const bool edge = c < lo || c + kChunk > hi;
-        if (edge || has_iv)
-            carry = count_chunk<K, true, GLOBAL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total);
+        if (ABL == 3) {          // profiling only: stream the bytes, no counting
+            lane_total += buf.x ^ buf.y ^ buf.z ^ buf.w;
+        } else if (edge || has_iv)
+            carry = count_chunk<K, true, GLOBAL, ABL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total);
         else
-            carry = count_chunk<K, false, GLOBAL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total);
+            carry = count_chunk<K, false, GLOBAL, ABL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total);
         c += kChunk;
     };
     // steady state: groups of 4 chunks with no exit in between (keeps the
@@ -404,9 +453,15 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
-template <int K>
-__global__ void __launch_bounds__(kBlock) count_kernel(CountArgs A) {
+template <int K, int V>
+__global__ void __launch_bounds__(Shape<V>::block)
+    __attribute__((amdgpu_waves_per_eu(Shape<V>::wpe ? Shape<V>::wpe : 1, Shape<V>::wpe ? Shape<V>::wpe : 8)))
+    count_kernel(CountArgs A) {
+    constexpr int kBlock = Shape<V>::block;
+    constexpr int kWaves = kBlock / kWave;
     constexpr bool GLOBAL = K > kLdsMaxK;
+    // dynamic LDS: the histogram at offset 0 (so bin addresses need no base add),
+    // then kWaves u64 reduction slots; no static __shared__ (it would precede it)
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
@@ -416,7 +471,7 @@ __global__ void __launch_bounds__(kBlock) count_kernel(CountArgs A) {
         for (uint32_t i = tid; i < NCODES; i += kBlock) hist[i] = 0;
         __syncthreads();
     }
-    __shared__ unsigned long long red[kWaves];
+    unsigned long long* red = (unsigned long long*)(hist + NCODES);
 
     const uint64_t base = A.goff[0];
     const uint64_t total = A.goff[A.n_genomes] - base;
@@ -449,7 +504,8 @@ __global__ void __launch_bounds__(kBlock) count_kernel(CountArgs A) {
             return min(max(s, plo), phi);
         };
         const uint64_t lo_c = split(wave), hi_c = split(wave + 1);
-        const uint64_t lt = process_range<K, GLOBAL>(A, g, glo, ghi, lo_c, hi_c, lane, hist);
+        const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl>(A, g, glo, ghi, lo_c, hi_c, lane, hist);
+        if (Shape<V>::abl) asm volatile("" ::"v"((uint32_t)lt));   // keep ablated work alive
         if (GLOBAL) {
             const unsigned long long s = wave_sum(lt);
             if (lane == 0 && s) atomicAdd(A.totals + g, s);
@@ -457,12 +513,15 @@ __global__ void __launch_bounds__(kBlock) count_kernel(CountArgs A) {
             __syncthreads();
             unsigned long long s = 0;
             uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
+            // canonical bin = forward count of the k-mer + forward count of its revcomp
             for (uint32_t col = tid; col < A.nbins; col += kBlock) {
                 const uint32_t rep = A.col2rep[col];
-                const uint32_t v = hist[rep];
+                const uint32_t rc = kf_revcomp<K>(rep);
+                const uint32_t v = hist[rep] + (rc != rep ? hist[rc] : 0u);
                 if (v) {
                     __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     hist[rep] = 0;
+                    hist[rc] = 0;
                     s += v;
                 }
             }
@@ -556,49 +615,67 @@ __global__ void __launch_bounds__(256) synth_kernel(uint8_t* bytes, const uint64
 using namespace kf;
 
 namespace {
-typedef void (*count_fn_t)(CountArgs);
+template <int K, int V>
+void* kernel_ptr() { return (void*)&count_kernel<K, V>; }
 
-template <int K>
-void* kernel_ptr() { return (void*)&count_kernel<K>; }
-
-void* count_kernel_for(int k) {
+template <int V>
+void* count_kernel_v(int k) {
     switch (k) {
-    case 2: return kernel_ptr<2>();
-    case 3: return kernel_ptr<3>();
-    case 4: return kernel_ptr<4>();
-    case 5: return kernel_ptr<5>();
-    case 6: return kernel_ptr<6>();
-    case 7: return kernel_ptr<7>();
-    case 8: return kernel_ptr<8>();
-    case 9: return kernel_ptr<9>();
-    case 10: return kernel_ptr<10>();
-    case 11: return kernel_ptr<11>();
-    case 12: return kernel_ptr<12>();
+    case 2: return kernel_ptr<2, V>();
+    case 3: return kernel_ptr<3, V>();
+    case 4: return kernel_ptr<4, V>();
+    case 5: return kernel_ptr<5, V>();
+    case 6: return kernel_ptr<6, V>();
+    case 7: return kernel_ptr<7, V>();
+    case 8: return kernel_ptr<8, V>();
+    case 9: return kernel_ptr<9, V>();
+    case 10: return kernel_ptr<10, V>();
+    case 11: return kernel_ptr<11, V>();
+    case 12: return kernel_ptr<12, V>();
     default: return nullptr;
     }
 }
 
-int lds_bytes_for(int k) { return k <= kLdsMaxK ? (int)(sizeof(uint32_t) << (2 * k)) : 0; }
+void* count_kernel_for(int k, int v) {
+#ifdef KF_ABLATION
+    if (v == 2) return count_kernel_v<2>(k);
+    if (v == 3) return count_kernel_v<3>(k);
+#endif
+    return v == 0 ? count_kernel_v<0>(k) : count_kernel_v<1>(k);
+}
+int block_for(int v) { return v == 0 ? Shape<0>::block : Shape<1>::block; }
+
+// KF_COUNT_VARIANT (tuning/A-B knob, read per launch): workgroup shape, see Shape<>.
+int current_variant() {
+    const char* e = getenv("KF_COUNT_VARIANT");
+    if (!e || !*e) return kDefaultVariant;
+    const int v = atoi(e);
+    return (v >= 0 && v < kNumVariants) ? v : kDefaultVariant;
+}
+
+// histogram (4^k u32) + one u64 reduction slot per wave (16 waves max)
+int lds_bytes_for(int k) { return k <= kLdsMaxK ? (int)(sizeof(uint32_t) << (2 * k)) + 16 * 8 : 0; }
 
 struct LaunchCache {
-    int grid[KF_MAX_K + 1][64];
+    int grid[KF_MAX_K + 1][kNumVariants][64];
 };
 LaunchCache g_cache = {};
 std::mutex g_cache_mu;
 
-int launch_info(int k, int* grid, int* block, int* lds) {
+int launch_info(int k, int* grid, int* block, int* lds, int* variant) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
     if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
+    const int v = current_variant();
     const int l = lds_bytes_for(k);
     std::lock_guard<std::mutex> lk(g_cache_mu);
-    int& gr = g_cache.grid[k][dev];
+    int& gr = g_cache.grid[k][v][dev];
     if (!gr) {
-        void* fn = count_kernel_for(k);
+        void* fn = count_kernel_for(k, v);
         if (l > 0 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, l) != hipSuccess)
             return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, l) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block_for(v), l) != hipSuccess)
             return kf_fail(KF_EHIP, "hipOccupancyMaxActiveBlocksPerMultiprocessor failed");
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return kf_fail(KF_EHIP, "hipDeviceGetAttribute(MultiprocessorCount) failed");
@@ -606,8 +683,9 @@ int launch_info(int k, int* grid, int* block, int* lds) {
         gr = per_cu * cus;
     }
     *grid = gr;
-    *block = kBlock;
+    *block = block_for(v);
     *lds = l;
+    *variant = v;
     return KF_OK;
 }
 }  // namespace
@@ -615,7 +693,8 @@ int launch_info(int k, int* grid, int* block, int* lds) {
 extern "C" int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes) {
     if (k < KF_MIN_K || k > KF_MAX_K) return kf_fail(KF_EINVAL, "k out of range [2, 12]");
     if (!grid || !block || !lds_bytes) return kf_fail(KF_EINVAL, "null output pointer");
-    return launch_info(k, grid, block, lds_bytes);
+    int v = 0;
+    return launch_info(k, grid, block, lds_bytes, &v);
 }
 
 extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
@@ -636,8 +715,8 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
             hipMemsetAsync(d_totals, 0, (size_t)n_genomes * sizeof(uint64_t), s) != hipSuccess)
             return kf_fail(KF_EHIP, "hipMemsetAsync failed");
     }
-    int grid = 0, block = 0, lds = 0;
-    int rc = launch_info(k, &grid, &block, &lds);
+    int grid = 0, block = 0, lds = 0, variant = 0;
+    int rc = launch_info(k, &grid, &block, &lds, &variant);
     if (rc) return rc;
     CountArgs A;
     A.bytes = d_bytes;
@@ -651,7 +730,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.nbins = (uint32_t)nb;
     A.n_genomes = n_genomes;
     void* args[] = {&A};
-    if (hipLaunchKernel(count_kernel_for(k), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
+    if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     return KF_OK;
 }

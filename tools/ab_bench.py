@@ -1,0 +1,71 @@
+"""Interleaved A/B timing of count-kernel variants in ONE process (guide §5.4 rule 24).
+
+  python tools/ab_bench.py --variants 0,1 --k 7 --rounds 5 --reps 5 [--genomes 1000]
+
+Each variant is selected with KF_COUNT_VARIANT; the batch (synthetic, device
+generated) is shared; outputs are compared bit-for-bit across variants.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--k", type=int, default=7)
+    ap.add_argument("--genomes", type=int, default=1000)
+    ap.add_argument("--seq-len", type=int, default=5_000_000)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--n-period", type=int, default=0)
+    args = ap.parse_args()
+    import torch
+    from kf2vecfsw_amd import counter as C
+    dev = torch.device("cuda:0")
+    db = C.synth_device_batch(args.genomes, args.seq_len, 20260101, n_period=args.n_period, device=dev)
+    kc = C.KmerCounter(args.k, dev)
+    fasta = int(db.off[-1].item())
+    variants = [int(v) for v in args.variants.split(",")]
+    times = {v: [] for v in variants}
+    ref = None
+    for r in range(args.rounds):
+        for v in variants:
+            os.environ["KF_COUNT_VARIANT"] = str(v)
+            cnt, tot = kc.alloc_out(args.genomes)
+            kc.count(db, cnt, tot)  # warm (also selects/caches the variant's grid)
+            torch.cuda.synchronize()
+            evs = []
+            for _ in range(args.reps):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                cnt.zero_()
+                tot.zero_()
+                a.record()
+                kc.count(db, cnt, tot, accumulate=True)
+                b.record()
+                evs.append((a, b))
+            torch.cuda.synchronize()
+            times[v] += [a.elapsed_time(b) for a, b in evs]
+            h = C.counts_to_numpy(cnt)
+            if ref is None:
+                ref = h
+            elif not np.array_equal(ref, h):
+                print(f"variant {v}: COUNTS DIFFER from variant {variants[0]}", flush=True)
+    out = {}
+    for v in variants:
+        t = np.array(times[v])
+        out[v] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+                  "GBps_median": fasta / (np.median(t) * 1e-3) / 1e9,
+                  "Gbases_s": args.genomes * args.seq_len / (np.median(t) * 1e-3) / 1e9,
+                  "grid": kc.launch_info() if False else None}
+    print(json.dumps({"k": args.k, "genomes": args.genomes, "bytes": fasta, "results": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
