@@ -169,6 +169,15 @@ __device__ __forceinline__ uint32_t run_mask(uint32_t E) {
     return R;
 }
 
+// Atomic add to the LDS word at byte address `a`.  The histogram is the whole
+// dynamic LDS allocation and the kernel declares no static LDS, so it starts at
+// LDS address 0 (checked once per kernel): a raw address-space-3 pointer avoids a
+// base add per k-mer.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ void lds_add(uint32_t a, uint32_t v) {
+    __hip_atomic_fetch_add((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t old, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
@@ -303,9 +312,14 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
     front_end<K, MASKED>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
 
     // context = own tail of lane L-1 (lane 0: carry), exact unless some lane is incomplete
+    // A block is incomplete (needs the exact scan) only if it has fewer than k-1
+    // entries and no reset; ne < k-1 needs >= 17-k newlines in 16 bytes, so test
+    // that first (one compare) and refine only when it fires.
     uint32_t ctx = wave_shr1(carry, own);
-    const uint64_t inc_mask = __ballot(!tail_complete<K>(own)) & 0x7FFFFFFFFFFFFFFFull;
-    if (inc_mask) ctx = scan_ctx<K>(own, carry, lane);
+    if (__ballot(ne < (uint32_t)(K - 1)) != 0) {
+        const uint64_t inc_mask = __ballot(!tail_complete<K>(own)) & 0x7FFFFFFFFFFFFFFFull;
+        if (inc_mask) ctx = scan_ctx<K>(own, carry, lane);
+    }
 
     const uint32_t ctxlen = min(t_n(ctx), (uint32_t)(K - 1));
     const uint64_t W = ((uint64_t)t_codes(ctx) << (2 * ne)) | (uint64_t)C;
@@ -324,22 +338,30 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
     if (!GLOBAL) {
         // LDS path: count FORWARD k-mers only into the 4^k histogram; a k-mer and
         // its reverse complement are merged into one canonical bin at flush time.
+        // Byte address of window r = 4*fwd(r) = bits [2r, 2r+2K+2) of X = W << 2,
+        // masked: 8 views at bit offsets 0,2,..,14 serve r = 0..7 from their low
+        // 16 bits and r = 8..15 from their high 16 bits (a word select).
+        constexpr uint32_t M4 = ((1u << W2) - 1u) << 2;
+        const uint32_t xlo = wlo << 2, xhi = __builtin_amdgcn_alignbit(whi, wlo, 30);
+        uint32_t xv[8];
+#pragma unroll
+        for (int o = 0; o < 8; ++o) xv[o] = o ? __builtin_amdgcn_alignbit(xhi, xlo, 2 * o) : xlo;
+        auto addr = [&](int r) -> uint32_t { return (r < 8 ? xv[r] : (xv[r - 8] >> 16)) & M4; };
         // Fast case (uniform): every window valid except possibly the 16th (a
         // newline in the block leaves 15 entries) -> no per-window inc extraction.
         const bool fast = !MASKED && __ballot((R | 0x8000u) != 0xFFFFu) == 0;
         if (ABL == 0 && fast) {
 #pragma unroll
-            for (int r = 0; r < 15; ++r)
-                __hip_atomic_fetch_add(hist + fwd(r), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(hist + fwd(15), R >> 15, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            for (int r = 0; r < 15; ++r) lds_add(addr(r), 1u);
+            lds_add(addr(15), R >> 15);
         } else {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const uint32_t inc = (R >> r) & 1u;
                 if (ABL == 0)
-                    __hip_atomic_fetch_add(hist + fwd(r), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    lds_add(addr(r), inc);
                 else   // profiling only (no LDS traffic)
-                    lane_total += fwd(r) ^ inc;
+                    lane_total += addr(r) ^ inc;
             }
         }
     } else {
@@ -472,6 +494,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
         __syncthreads();
     }
     unsigned long long* red = (unsigned long long*)(hist + NCODES);
+    if (!GLOBAL && (uint32_t)(uintptr_t)(lds_u32*)hist != 0u) __builtin_trap();   // lds_add assumes base 0
 
     const uint64_t base = A.goff[0];
     const uint64_t total = A.goff[A.n_genomes] - base;
