@@ -49,7 +49,23 @@ template <> struct Shape<1> { static constexpr int block = 1024, wpe = 8, abl = 
 template <> struct Shape<2> { static constexpr int block = 1024, wpe = 8, abl = 1; };   // no LDS adds
 template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 3; };   // stream bytes only
 #endif
-constexpr int kLdsMaxK = 7;        // 4^7 x 4 B = 64 KiB histogram
+// Counting modes by k:
+//   k <= 7 : one LDS histogram of all 4^k forward codes (64 KiB at k=7)
+//   k 8..9 : multi-pass LDS: the forward-code space is cut into 32768-code
+//            ranges (128 KiB of LDS); pass p counts codes with code >> 15 == p
+//            and its flush merges into the canonical columns (2 / 8 passes)
+//   k >= 10: global atomics at code2col[min(fwd, revcomp)]
+constexpr int kLdsMaxK = 7;
+constexpr int kMultiMaxK = 9;
+constexpr int kMultiBits = 15;
+enum { kModeLds = 0, kModeMulti = 1, kModeGlobal = 2 };
+template <int K>
+struct ModeOf {
+    static constexpr int mode = K <= kLdsMaxK ? kModeLds : (K <= kMultiMaxK ? kModeMulti : kModeGlobal);
+    static constexpr int passes = mode == kModeMulti ? (1 << (2 * K - kMultiBits)) : 1;
+    static constexpr uint32_t lds_codes = mode == kModeLds ? (1u << (2 * K))
+                                        : (mode == kModeMulti ? (1u << kMultiBits) : 0u);
+};
 
 struct CountArgs {
     const uint8_t* bytes;
@@ -305,7 +321,7 @@ template <int K, bool MASKED, bool GLOBAL, int ABL>
 __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
                                                 const ChunkMask& m, uint64_t iv0, uint32_t carry,
                                                 uint32_t* __restrict__ hist, uint32_t* __restrict__ gcounts,
-                                                uint32_t& lane_total) {
+                                                uint32_t& lane_total, uint32_t pass) {
     constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
     constexpr int W2 = 2 * K;
     uint32_t C, V, EN, ne, own;
@@ -335,7 +351,14 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
         const int fo = (2 * r) & ~7;
         return __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, W2);
     };
-    if (!GLOBAL) {
+    if (ModeOf<K>::mode == kModeMulti) {
+        // multi-pass LDS: this pass counts forward codes in [pass << 15, (pass+1) << 15)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t f = fwd(r);
+            if (((R >> r) & 1u) && (f >> kMultiBits) == pass) lds_add((f & ((1u << kMultiBits) - 1u)) << 2, 1u);
+        }
+    } else if (!GLOBAL) {
         // LDS path: count FORWARD k-mers only into the 4^k histogram; a k-mer and
         // its reverse complement are merged into one canonical bin at flush time.
         // Byte address of window r = 4*fwd(r) = bits [2r, 2r+2K+2) of X = W << 2,
@@ -394,7 +417,7 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
 template <int K, bool GLOBAL, int ABL>
 __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                   uint64_t lo, uint64_t hi, int lane,
-                                                  uint32_t* __restrict__ hist) {
+                                                  uint32_t* __restrict__ hist, uint32_t pass) {
     uint64_t c = lo & ~(uint64_t)15;
     if (lo >= hi) return 0;
     uint32_t* gcounts = GLOBAL ? A.counts + (uint64_t)g * A.nbins : nullptr;
@@ -444,9 +467,9 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
         if (ABL == 3) {          // profiling only: stream the bytes, no counting
             lane_total += buf.x ^ buf.y ^ buf.z ^ buf.w;
         } else if (edge || has_iv)
-            carry = count_chunk<K, true, GLOBAL, ABL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total);
+            carry = count_chunk<K, true, GLOBAL, ABL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total, pass);
         else
-            carry = count_chunk<K, false, GLOBAL, ABL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total);
+            carry = count_chunk<K, false, GLOBAL, ABL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total, pass);
         c += kChunk;
     };
     // steady state: groups of 4 chunks with no exit in between (keeps the
@@ -481,14 +504,15 @@ __global__ void __launch_bounds__(Shape<V>::block)
     count_kernel(CountArgs A) {
     constexpr int kBlock = Shape<V>::block;
     constexpr int kWaves = kBlock / kWave;
-    constexpr bool GLOBAL = K > kLdsMaxK;
+    constexpr bool GLOBAL = ModeOf<K>::mode == kModeGlobal;
+    constexpr bool MULTI = ModeOf<K>::mode == kModeMulti;
     // dynamic LDS: the histogram at offset 0 (so bin addresses need no base add),
     // then kWaves u64 reduction slots; no static __shared__ (it would precede it)
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    constexpr uint32_t NCODES = 1u << (2 * (GLOBAL ? 1 : K));
+    constexpr uint32_t NCODES = GLOBAL ? 4u : ModeOf<K>::lds_codes;
     if (!GLOBAL) {
         for (uint32_t i = tid; i < NCODES; i += kBlock) hist[i] = 0;
         __syncthreads();
@@ -527,35 +551,56 @@ __global__ void __launch_bounds__(Shape<V>::block)
             return min(max(s, plo), phi);
         };
         const uint64_t lo_c = split(wave), hi_c = split(wave + 1);
-        const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl>(A, g, glo, ghi, lo_c, hi_c, lane, hist);
-        if (Shape<V>::abl) asm volatile("" ::"v"((uint32_t)lt));   // keep ablated work alive
         if (GLOBAL) {
+            const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
             const unsigned long long s = wave_sum(lt);
             if (lane == 0 && s) atomicAdd(A.totals + g, s);
-        } else {
+            continue;
+        }
+        unsigned long long s = 0;
+        uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
+        for (uint32_t pass = 0; pass < (uint32_t)ModeOf<K>::passes; ++pass) {
+            const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl>(A, g, glo, ghi, lo_c, hi_c, lane, hist, pass);
+            if (Shape<V>::abl) asm volatile("" ::"v"((uint32_t)lt));   // keep ablated work alive
             __syncthreads();
-            unsigned long long s = 0;
-            uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
-            // canonical bin = forward count of the k-mer + forward count of its revcomp
+            // canonical bin = forward count of the k-mer + forward count of its
+            // revcomp; coalesced u32 atomics in column order
             for (uint32_t col = tid; col < A.nbins; col += kBlock) {
                 const uint32_t rep = A.col2rep[col];
                 const uint32_t rc = kf_revcomp<K>(rep);
-                const uint32_t v = hist[rep] + (rc != rep ? hist[rc] : 0u);
+                uint32_t v;
+                if (!MULTI) {
+                    v = hist[rep] + (rc != rep ? hist[rc] : 0u);
+                    if (v) {
+                        hist[rep] = 0;
+                        hist[rc] = 0;
+                    }
+                } else {
+                    constexpr uint32_t M = (1u << kMultiBits) - 1u;
+                    v = 0;
+                    if ((rep >> kMultiBits) == pass) {
+                        v += hist[rep & M];
+                        hist[rep & M] = 0;
+                    }
+                    if (rc != rep && (rc >> kMultiBits) == pass) {
+                        v += hist[rc & M];
+                        hist[rc & M] = 0;
+                    }
+                }
                 if (v) {
                     __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    hist[rep] = 0;
-                    hist[rc] = 0;
                     s += v;
                 }
             }
-            s = wave_sum(s);
-            if (lane == 0) red[wave] = s;
             __syncthreads();
-            if (tid == 0) {
-                unsigned long long t = 0;
-                for (int w = 0; w < kWaves; ++w) t += red[w];
-                if (t) atomicAdd(A.totals + g, t);
-            }
+        }
+        s = wave_sum(s);
+        if (lane == 0) red[wave] = s;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long t = 0;
+            for (int w = 0; w < kWaves; ++w) t += red[w];
+            if (t) atomicAdd(A.totals + g, t);
         }
     }
 }
@@ -677,7 +722,11 @@ int current_variant() {
 }
 
 // histogram (4^k u32) + one u64 reduction slot per wave (16 waves max)
-int lds_bytes_for(int k) { return k <= kLdsMaxK ? (int)(sizeof(uint32_t) << (2 * k)) + 16 * 8 : 0; }
+int lds_bytes_for(int k) {
+    if (k <= kLdsMaxK) return (int)(sizeof(uint32_t) << (2 * k)) + 16 * 8;
+    if (k <= kMultiMaxK) return (int)(sizeof(uint32_t) << kMultiBits) + 16 * 8;
+    return 0;
+}
 
 struct LaunchCache {
     int grid[KF_MAX_K + 1][kNumVariants][64];
