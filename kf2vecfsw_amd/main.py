@@ -122,13 +122,173 @@ def get_frequencies(args) -> None:
     print("\n==> Done processing {}".format(args.input_dir))
 
 
+# ---------------------------------------------------------------------------
+# get_kmers (main.py:112-184): sparse present-k-mer matrices for the FSW trainer
+# ---------------------------------------------------------------------------
+_GET_KMERS_DIGIT = {ord("A"): 0, ord("T"): 1, ord("C"): 2, ord("G"): 3}   # main.py:118
+_digit_tables: dict = {}
+
+
+def vocab_digits(k: int) -> np.ndarray:
+    """uint8 [nbins, k]: the vocab k-mers as get_kmers digits (A0 T1 C2 G3)."""
+    if k not in _digit_tables:
+        from .counter import vocab_text
+        v = np.frombuffer(vocab_text(k), dtype=np.uint8).reshape(-1, k + 1)[:, :k]
+        lut = np.zeros(256, dtype=np.uint8)
+        for ch, d in _GET_KMERS_DIGIT.items():
+            lut[ch] = d
+        _digit_tables[k] = lut[v]
+    return _digit_tables[k]
+
+
+def kmers_matrix(counts: np.ndarray, k: int) -> np.ndarray:
+    """float32 [n_present, k+1]: digits of each present canonical k-mer + count /
+    total (main.py:165-172).  Rows in vocab (sorted canonical) order; the
+    reference's rows follow Jellyfish's hash order, which its FSW consumer
+    (models.py:60-64) does not depend on.  With < 2^24 k-mers the float32 sum
+    is exact in any order, so the weights equal the reference's bit for bit."""
+    counts = np.asarray(counts)
+    nz = np.nonzero(counts)[0]
+    if nz.size == 0:
+        return np.zeros((0, k + 1), dtype=np.float32)
+    c = counts[nz].astype(np.float32)
+    norm = c / np.sum(c)
+    return np.column_stack((vocab_digits(k)[nz].astype(np.float32), norm))
+
+
+def get_kmers(args) -> None:
+    """kf2vec/main.py:112-184 on the GPU (all *.fna of input_dir in one batch)."""
+    import glob
+
+    import torch
+    from .counter import KmerCounter, counts_to_numpy, pack_files, to_device
+
+    if not os.path.exists(args.output_dir):             # main.py:121-122
+        os.makedirs(args.output_dir)
+    fasta_files = glob.glob(os.path.join(args.input_dir, "*.fna"))   # main.py:124
+    if not fasta_files:
+        return
+    device = torch.device(getattr(args, "device", None) or "cuda")
+    counter = KmerCounter(args.k, device)
+    budget = int(float(getattr(args, "batch_gb", 4.0) or 4.0) * (1 << 30))
+    for idx in _batches(fasta_files, budget):
+        paths = [fasta_files[i] for i in idx]
+        names = [os.path.basename(p).replace(".fna", "") for p in paths]   # main.py:127
+        counts, _ = counter.count(to_device(pack_files(paths, names), device))
+        c = counts_to_numpy(counts)
+        for j, base_name in enumerate(names):
+            print(f"--- Processing {base_name} ---")
+            m = kmers_matrix(c[j], args.k)
+            if m.shape[0] == 0:
+                print(f"Warning: No valid ATCG k-mers found in {base_name}")
+                continue
+            output_path = os.path.join(args.output_dir, f"{base_name}_k{args.k}.npy")
+            np.save(output_path, m)
+            print(f"Saved: {output_path} (Shape: {m.shape})")
+
+
+# ---------------------------------------------------------------------------
+# get_chunks (main.py:654-929): raw-count rows of 10 kbp windows per genome
+# ---------------------------------------------------------------------------
+def _hms(seconds: float) -> tuple[int, int, int]:
+    m, s = divmod(int(seconds), 60)
+    h, m = divmod(m, 60)
+    return h, m, s
+
+
+def get_chunks(args) -> None:
+    """kf2vec/main.py:654-929: one device batch of all windows of a group of
+    genomes instead of one Jellyfish pair per 10 kbp window."""
+    import logging
+    import time
+
+    import torch
+    from . import chunks as CH
+    from .counter import KmerCounter, counts_to_numpy, pack_genomes, to_device
+
+    since = time.time()
+    if not os.path.exists(args.input_dir):
+        print("No such directory '{}'".format(args.input_dir), file=sys.stderr)
+        sys.exit(0)
+    if not os.path.exists(args.output_dir):
+        print("No such directory '{}'".format(args.output_dir), file=sys.stderr)
+        sys.exit(0)
+    log = logging.getLogger("kf2vecfsw_amd.get_chunks")
+    log.setLevel(logging.INFO)
+    log.handlers[:] = [logging.FileHandler(os.path.join(args.output_dir, "get_chunks_{}.log".format(
+        os.path.basename(os.path.normpath(args.input_dir)))), "w+"), logging.StreamHandler(sys.stdout)]
+    for h in log.handlers:
+        h.setFormatter(logging.Formatter("%(message)s"))
+
+    def stamp(msg):
+        hrs, _min, sec = _hms(time.time() - since)
+        log.info(msg + " Time: {:02d}:{:02d}:{:02d}\n".format(hrs, _min, sec))
+
+    stamp("\n==> Making a list of sample names.")
+    files_names, samples_names = list_inputs(args.input_dir)
+    stamp("\n==> Start processing samples.")
+    if args.k not in supported_k:
+        raise ValueError("k={} has no vocabulary: supported k are {}..{}".format(
+            args.k, supported_k.start, supported_k.stop - 1))
+    device = torch.device(getattr(args, "device", None) or "cuda")
+    counter = KmerCounter(args.k, device)
+    budget = int(float(getattr(args, "batch_gb", 4.0) or 4.0) * (1 << 30))
+
+    pending: list[tuple[str, list[tuple[str, bytes]]]] = []
+    pending_bytes = 0
+
+    def flush_pending():
+        nonlocal pending, pending_bytes
+        if not pending:
+            return
+        blobs, names = [], []
+        for _, wins in pending:
+            for nm, seq in wins:
+                names.append(nm)
+                blobs.append(seq)
+        counts, _ = counter.count(to_device(pack_genomes(blobs, names), device))
+        c = counts_to_numpy(counts)
+        row = 0
+        for sample, wins in pending:
+            lines = [format_kf(nm, c[row + j], args.pseudocount, True) for j, (nm, _) in enumerate(wins)]
+            row += len(wins)
+            with open(os.path.join(args.output_dir, "{}.kf".format(sample)), "wb") as f:
+                f.write(b"".join(lines))
+            stamp("\n==> Done computing k-mer frequences for {}.".format(
+                dict((s, fn) for fn, s in zip(files_names, samples_names)).get(sample, sample)))
+        pending, pending_bytes = [], 0
+
+    for fname, sample in zip(files_names, samples_names):
+        log.info("\n==> Start processing. Sample: {}".format(fname))
+        with open(os.path.join(args.input_dir, fname), "rb") as f:
+            data = f.read()
+        wins = CH.genome_windows(data, sample)
+        if not wins:   # no contig of >= 10 kbp after N-collapse / gap removal (main.py:761-778)
+            stamp("\n==> Excluded {}. No contigs above threshold length.".format(fname))
+            continue
+        if len(wins) < CH.CHUNK_CNT_THR:                                   # main.py:845-860
+            stamp("\n==> Excluded {}. {} chunks is too low. {} is required.".format(
+                fname, len(wins), CH.CHUNK_CNT_THR))
+            continue
+        stamp("\n==> Done chunk processing for {}.".format(fname))
+        pending.append((sample, wins))
+        pending_bytes += len(wins) * CH.CHUNK_SZ
+        if pending_bytes >= budget:
+            flush_pending()
+    flush_pending()
+    stamp("\n==> Done getting chunks.")
+
+
 def build_parser() -> argparse.ArgumentParser:
     parser = argparse.ArgumentParser(description="K-mer frequency to distance\n{}".format(__version__),
                                      formatter_class=argparse.RawDescriptionHelpFormatter)
     parser.add_argument("-v", "--version", action="version", version="{}".format(__version__))
     sub = parser.add_subparsers(title="commands", dest="{commands}",
-                                description="get_frequencies          Extract k-mer frequency from a reference "
-                                            "genome-skims or assemblies\n")
+                                description="get_kmers                Extract k-mers and their frequencies from "
+                                            "FASTA files\n"
+                                            "get_frequencies          Extract k-mer frequency from a reference "
+                                            "genome-skims or assemblies\n"
+                                            "get_chunks               Extract chunks from reference assemblies\n")
     pf = sub.add_parser("get_frequencies", description="Process a library of reference genome-skims or assemblies")
     pf.add_argument("-input_dir", help="Directory of input genomes or assemblies "
                                        "(dir of .fastq/.fq/.fa/.fna/.fasta files)")
@@ -145,6 +305,29 @@ def build_parser() -> argparse.ArgumentParser:
     pf.add_argument("-batch_gb", type=float, default=4.0, help="Input bytes per device batch (GiB). Default: 4")
     pf.add_argument("-device", default=None, help="torch device (default: cuda)")
     pf.set_defaults(func=get_frequencies)
+
+    pk = sub.add_parser("get_kmers", description="Extract kmers and frequencies from FASTA files")
+    pk.add_argument("-input_dir", help="Directory of input genomes or assemblies (dir of .fna files)")
+    pk.add_argument("-output_dir", help="Directory for k-mer outputs (.npy files)")
+    pk.add_argument("-k", type=int, choices=list(range(N.KF_MIN_K, N.KF_MAX_K + 1)), default=default_k_len,
+                    help="K-mer length. Default: {}".format(default_k_len), metavar="K")
+    pk.add_argument("-batch_gb", type=float, default=4.0, help="Input bytes per device batch (GiB)")
+    pk.add_argument("-device", default=None, help="torch device (default: cuda)")
+    pk.set_defaults(func=get_kmers)
+
+    pc = sub.add_parser("get_chunks", description="Extract chunks from reference assemblies")
+    pc.add_argument("-input_dir", help="Directory of input genomes or assemblies")
+    pc.add_argument("-output_dir", help="Directory for chunked k-mer counts (.kf files)")
+    pc.add_argument("-k", type=int, choices=list(range(min_k_len, max_k_len + 1)), default=default_k_len,
+                    help="K-mer length [{}-{}]. Default: {}".format(min_k_len, max_k_len, default_k_len),
+                    metavar="K")
+    pc.add_argument("-p", type=int, choices=list(range(1, mp.cpu_count() + 1)), default=mp.cpu_count(),
+                    help="Max number of processors to use", metavar="P")
+    pc.add_argument("-pseudocount", action="store_true",
+                    help="Computes k-mer counts with 0.5 pseudocount added to each frequency value")
+    pc.add_argument("-batch_gb", type=float, default=1.0, help="Window bytes per device batch (GiB)")
+    pc.add_argument("-device", default=None, help="torch device (default: cuda)")
+    pc.set_defaults(func=get_chunks)
     return parser
 
 

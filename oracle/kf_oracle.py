@@ -163,6 +163,8 @@ def fasta_records(data: bytes) -> list[tuple[str, bytes]]:
     recs = []
     name, seq = None, []
     for line in data.split(b"\n"):
+        if line.endswith(b"\r"):     # seqtk's kseq strips a trailing CR
+            line = line[:-1]
         if line.startswith(b">"):
             if name is not None:
                 recs.append((name, b"".join(seq)))
@@ -175,6 +177,7 @@ def fasta_records(data: bytes) -> list[tuple[str, bytes]]:
 
 
 _NRUN = re.compile(rb"[N|n]+")   # awk gsub(/[N|n]+/,"N") (main.py:740) -- '|' included
+_GAPS = re.compile(rb"[- \t.]")  # seqkit seq -g default gap letters
 
 
 def chunk_windows(fna: bytes, sample: str) -> list[tuple[str, bytes]]:
@@ -184,7 +187,7 @@ def chunk_windows(fna: bytes, sample: str) -> list[tuple[str, bytes]]:
     out = []
     for hdr, seq in fasta_records(fna):
         seq = _NRUN.sub(b"N", seq)                     # main.py:740-742
-        seq = seq.replace(b"-", b"")                   # seqkit seq -g (remove gaps)
+        seq = _GAPS.sub(b"", seq)                      # seqkit seq -g (gap letters "- \\t.")
         if len(seq) < CHUNK_SZ:                        # seqkit seq -m 10000 (main.py:753)
             continue
         cid = hdr.split()[0]
@@ -199,3 +202,32 @@ def chunk_windows(fna: bytes, sample: str) -> list[tuple[str, bytes]]:
             out.append((name, seq[s:s + CHUNK_SZ]))
             s += step
     return out
+
+
+# ---------------------------------------------------------------------------
+# get_kmers (kf2vec/main.py:112-184): sparse present-k-mer matrix for FSW
+# ---------------------------------------------------------------------------
+GET_KMERS_CODE = {ord("A"): 0, ord("T"): 1, ord("C"): 2, ord("G"): 3}   # main.py:118
+
+
+def kmers_matrix_from_dump(dump_lines: list[tuple[str, int]], k: int) -> np.ndarray:
+    """Restates main.py:147-172 for `jellyfish dump -c -t` lines (kmer, count) in
+    whatever order Jellyfish emits them: rows = k digits (A0 T1 C2 G3) + float32
+    count / float32 sum."""
+    kmer_data, counts = [], []
+    for seq, cnt in dump_lines:
+        if all(b in "ATCG" for b in seq):                        # main.py:154
+            kmer_data.append([GET_KMERS_CODE[ord(b)] for b in seq])   # :156
+            counts.append(int(cnt))
+    if not kmer_data:
+        return np.zeros((0, k + 1), dtype=np.float32)
+    kmer_matrix = np.array(kmer_data, dtype=np.float32)            # :165
+    counts_array = np.array(counts, dtype=np.float32)              # :166
+    normalized = counts_array / np.sum(counts_array)               # :169
+    return np.column_stack((kmer_matrix, normalized))             # :172
+
+
+def dump_lines(counts: np.ndarray, k: int) -> list[tuple[str, int]]:
+    """The `jellyfish dump -c` content implied by a count vector (vocab order)."""
+    vocab = vocab_text(k).split()
+    return [(vocab[i].decode(), int(c)) for i, c in enumerate(counts) if c]

@@ -210,3 +210,39 @@ def test_genome_end_at_every_alignment(torch_dev, oracle):
     for k in (3, 7, 11):
         counts, totals = run_batch(blobs, k, torch_dev, offsets=off)
         check_against_oracle(oracle, blobs, k, counts, totals, tag="end-align")
+
+
+def test_cli_get_chunks_matches_reference_chunk_files(torch_dev, tmp_path):
+    """`get_chunks` (GPU windows, raw counts) reproduces the committed chunk `.kf`
+    rows of toy_example/train_tree_chunks byte for byte (row order across contigs
+    is os.listdir-dependent in the reference, so rows are compared by name)."""
+    from conftest import TOY
+    from kf2vecfsw_amd import main as M
+    inp, out = tmp_path / "in", tmp_path / "out"
+    inp.mkdir()
+    out.mkdir()
+    for f in sorted(os.listdir(os.path.join(TOY, "train_tree_fna"))):
+        (inp / f[:-3]).write_bytes(gzip.open(os.path.join(TOY, "train_tree_fna", f)).read())
+    M.main(["get_chunks", "-input_dir", str(inp), "-output_dir", str(out), "-k", "7"])
+    n_rows = 0
+    for f in sorted(os.listdir(os.path.join(TOY, "train_tree_chunks"))):
+        exp = gzip.open(os.path.join(TOY, "train_tree_chunks", f)).read().decode().splitlines(True)
+        got = (out / f[:-3]).read_text().splitlines(True)
+        assert sorted(got) == sorted(exp), f
+        n_rows += len(exp)
+    assert n_rows == 358
+
+
+def test_cli_get_kmers_matches_oracle(torch_dev, toy, oracle, tmp_path):
+    """`get_kmers` .npy == main.py:147-172 restated on the oracle's counts."""
+    from kf2vecfsw_amd import main as M
+    inp, out = tmp_path / "in", tmp_path / "out"
+    inp.mkdir()
+    for name, sample, data, exp in toy:
+        (inp / name).write_bytes(data)
+    M.main(["get_kmers", "-input_dir", str(inp), "-output_dir", str(out), "-k", "7"])
+    for name, sample, data, exp in toy:
+        m = np.load(out / f"{sample}_k7.npy")
+        c, _ = oracle.count(data, 7)
+        ref = oracle.kmers_matrix_from_dump(oracle.dump_lines(c, 7), 7)
+        assert m.dtype == np.float32 and np.array_equal(m, ref), sample

@@ -135,3 +135,36 @@ def test_count_batch_rejects_bad_args(native):
     assert L.kf_count_batch(None, None, 1, None, 0, None, None, 13, None, None, 0, None) == N.KF_EINVAL
     assert b"k out of range" in L.kf_last_error()
     assert L.kf_count_batch(None, None, 0, None, 0, None, None, 7, None, None, 0, None) == N.KF_OK
+
+
+def test_chunk_window_plan_matches_oracle(oracle):
+    """Host window plan of get_chunks (product) == oracle restatement, on the toy genomes."""
+    from kf2vecfsw_amd import chunks as CH
+    for f in sorted(os.listdir(os.path.join(TOY, "train_tree_fna"))):
+        data = gzip.open(os.path.join(TOY, "train_tree_fna", f)).read()
+        sample = f[:-3].rsplit(".f", 1)[0]
+        a = CH.genome_windows(data, sample)
+        b = oracle.chunk_windows(data, sample)
+        assert [x[0] for x in a] == [x[0] for x in b]
+        assert all(x[1] == y[1] for x, y in zip(a, b))
+    for L in [9999, 10000, 10001, 19999, 20000, 25000, 1241422]:
+        n, step = CH.window_plan(L)
+        assert n == (0 if L < 10000 else len(range(0, L - 10000 + 1, step)))
+
+
+def test_get_kmers_matrix_matches_reference_restatement(native, oracle):
+    """kmers_matrix (product) == main.py:147-172 restated, fed the dump implied by the counts."""
+    from kf2vecfsw_amd.main import kmers_matrix
+    data = gzip.open(os.path.join(TOY, "test_fna", "G000830275sub.fna.gz")).read()
+    for k in (3, 7, 9):
+        c, _ = oracle.count(data, k)
+        got = kmers_matrix(c, k)
+        exp = oracle.kmers_matrix_from_dump(oracle.dump_lines(c, k), k)
+        assert got.dtype == np.float32 and got.shape == exp.shape
+        assert np.array_equal(got, exp)
+        # permutation invariance: a shuffled dump gives the same rows (as a set)
+        lines = oracle.dump_lines(c, k)
+        rng = np.random.default_rng(k)
+        shuf = oracle.kmers_matrix_from_dump([lines[i] for i in rng.permutation(len(lines))], k)
+        key = lambda m: m[np.lexsort(m[:, ::-1].T)]
+        assert np.array_equal(key(got), key(shuf))
