@@ -124,21 +124,33 @@ def pack_genomes(blobs: Sequence[bytes | np.ndarray], names: Sequence[str] | Non
 
 
 def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: int = N.KF_FMT_AUTO,
-               pin: bool = True) -> HostBatch:
+               pin: bool = True, threads: int = 8) -> HostBatch:
+    """Read files straight into one (pinned) buffer and index their records; files
+    are read and indexed by a thread pool (readinto and the ctypes call release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
     sizes = [os.path.getsize(p) for p in paths]
     off = _layout(sizes)
     data = _alloc_host(int(off[-1]), pin)
     d = data.numpy()
-    excl = []
-    for i, p in enumerate(paths):
+
+    def one(i: int) -> np.ndarray:
         lo, sz = int(off[i]), sizes[i]
-        with open(p, "rb", buffering=0) as f:
-            got = f.readinto(memoryview(d[lo: lo + sz]))
-        if got != sz:
-            raise IOError(f"short read on {p}")
+        with open(paths[i], "rb", buffering=0) as f:
+            got = 0
+            mv = memoryview(d[lo: lo + sz])
+            while got < sz:
+                n = f.readinto(mv[got:])
+                if not n:
+                    raise IOError(f"short read on {paths[i]}")
+                got += n
         d[lo + sz: int(off[i + 1])] = 10
-        iv, _ = index_records(d[lo: lo + sz], fmt, lo)
-        excl.append(iv)
+        return index_records(d[lo: lo + sz], fmt, lo)[0]
+
+    if threads > 1 and len(paths) > 1:
+        with ThreadPoolExecutor(max_workers=min(threads, len(paths))) as ex:
+            excl = list(ex.map(one, range(len(paths))))
+    else:
+        excl = [one(i) for i in range(len(paths))]
     ex = np.concatenate(excl) if excl else np.zeros(0, np.uint64)
     return HostBatch(data, off, ex.astype(np.uint64), list(names) if names else list(paths))
 

@@ -103,8 +103,20 @@ def get_frequencies(args) -> None:
     # the reference processes files in order and later ones overwrite earlier
     # ones with the same sample name: keep the last occurrence only
     last = {s: i for i, s in enumerate(samples_names)}
-    for idx in _batches(paths, budget):
-        hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx])
+    batches = _batches(paths, budget)
+    threads = max(1, int(args.p))
+    from concurrent.futures import ThreadPoolExecutor
+
+    def pack(idx):
+        return pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], threads=threads)
+
+    # pipeline: the next batch is read + indexed while this one is counted and written
+    prefetch = ThreadPoolExecutor(max_workers=1)
+    fut = prefetch.submit(pack, batches[0]) if batches else None
+    for bi, idx in enumerate(batches):
+        hb = fut.result()
+        if bi + 1 < len(batches):
+            fut = prefetch.submit(pack, batches[bi + 1])
         db = to_device(hb, device)
         counts, _ = counter.count(db)
         c = counts_to_numpy(counts)
@@ -118,6 +130,7 @@ def get_frequencies(args) -> None:
                 keep.append(j)
         write_kf_files(args.output_dir, [samples_names[idx[j]] for j in keep], c[keep],
                        args.pseudocount, args.raw_cnt, args.p)
+    prefetch.shutdown()
 
     print("\n==> Done processing {}".format(args.input_dir))
 
