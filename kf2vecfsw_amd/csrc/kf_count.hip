@@ -107,33 +107,38 @@ __device__ __forceinline__ bool tail_complete(uint32_t t) {
 }
 
 // ---------------------------------------------------------------- classify
-// 16 bytes -> codes C (byte i at bits 2(15-i)), invalid mask INV and newline
-// mask NL (byte i at bit 15-i).  Valid bases: ACGTacgt.
+// 16 bytes -> codes C (byte i at bits 2(15-i)), invalid mask INV and
+// not-newline mask NNL (byte i at bit 15-i).  Valid bases: ACGTacgt.
 //   cb = (b >> 1) & 3            kf code (A0 C1 T2 G3)
 //   y  = (b ^ TBL[cb]) & 0xDF    == 0x0C iff b is the base cb (either case)
 //   perm(-1,-1,sel) yields 0x00 for sel == 12 and 0xFF for every other byte
 //   dot4 packs four codes / four flags into one byte / nibble in memory order.
-__device__ __forceinline__ void classify16(const uint4 d, uint32_t& C, uint32_t& INV, uint32_t& NL) {
+__device__ __forceinline__ void classify16(const uint4 d, uint32_t& C, uint32_t& INV, uint32_t& NNL) {
     const uint32_t w[4] = {d.x, d.y, d.z, d.w};
-    uint32_t pc[4];
-    int pv[4], pn[4];   // flag nibbles
+    uint32_t pc[4], vf[4], nf[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t x = w[q];
         const uint32_t cb = (x >> 1) & 0x03030303u;
         const uint32_t ex = __builtin_amdgcn_perm(0u, 0x4B584F4Du, cb);   // "ACTG" ^ 0x0C
         const uint32_t y = (x ^ ex) & 0xDFDFDFDFu;
-        const uint32_t vf = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, y);
-        const uint32_t nf = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, x ^ 0x06060606u);
+        vf[q] = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, y);          // 0x00 valid base
+        nf[q] = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, x ^ 0x06060606u);   // 0x00 newline
         pc[q] = __builtin_amdgcn_udot4(cb, 0x01041040u, 0u, false);
-        // flag bytes are 0x00 / 0xFF (= -1 signed); weights -8,-4,-2,-1 give the
-        // positive nibble directly (no negation, no multiply in the combine)
-        pv[q] = __builtin_amdgcn_sdot4((int)vf, (int)0xFFFEFCF8u, 0, false);
-        pn[q] = __builtin_amdgcn_sdot4((int)nf, (int)0xFFFEFCF8u, 0, false);
     }
-    C = (pc[0] << 24) | (pc[1] << 16) | (pc[2] << 8) | pc[3];
-    INV = ((uint32_t)pv[0] << 12) | ((uint32_t)pv[1] << 8) | ((uint32_t)pv[2] << 4) | (uint32_t)pv[3];
-    NL = 0xFFFFu ^ (((uint32_t)pn[0] << 12) | ((uint32_t)pn[1] << 8) | ((uint32_t)pn[2] << 4) | (uint32_t)pn[3]);
+    // codes: byte q of C (from the top) = pc[q]
+    const uint32_t c01 = __builtin_amdgcn_perm(pc[0], pc[1], 0x0C0C0400u);
+    const uint32_t c23 = __builtin_amdgcn_perm(pc[2], pc[3], 0x0C0C0400u);
+    C = (c01 << 16) | c23;
+    // flag bytes are 0x00 / 0xFF (= -1 signed).  Weights -8,-4,-2,-1 give dword
+    // q+1's nibble and -128,-64,-32,-16 dword q's nibble one position up, so one
+    // accumulating dot pair packs a byte of the mask.
+    auto pair = [](const uint32_t a, const uint32_t b) -> uint32_t {
+        return (uint32_t)__builtin_amdgcn_sdot4((int)a, (int)0xF0E0C080u,
+                                               __builtin_amdgcn_sdot4((int)b, (int)0xFFFEFCF8u, 0, false), false);
+    };
+    INV = (pair(vf[0], vf[1]) << 8) | pair(vf[2], vf[3]);
+    NNL = (pair(nf[0], nf[1]) << 8) | pair(nf[2], nf[3]);   // not-newline mask
 }
 
 // Remove newline entries (compaction).  C: 2-bit entries, V/EN: 1-bit masks,
@@ -255,34 +260,38 @@ __device__ __forceinline__ void apply_masks(const CountArgs& A, uint64_t chunk, 
 // 16 bytes: the hardware range check zeroes a whole dword/vector that straddles
 // num_records, so an exact (unaligned) end would drop the genome's last bases.
 // Bytes in [ghi, align16(ghi)) are read but never counted (they lie past hi).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const uint8_t* bytes, uint64_t c, uint64_t ghi) {
-    const uint64_t end = (ghi + 15) & ~(uint64_t)15;
-    const uint32_t rec = c >= end ? 0u : (uint32_t)min<uint64_t>(end - c, (uint64_t)kChunk);
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c), (short)0, (int)rec, 0x00020000);
-}
-
-__device__ __forceinline__ uint4 load_chunk(const uint8_t* bytes, uint64_t c, uint64_t ghi, int lane) {
-    const auto rs = chunk_rsrc(bytes, c, ghi);
+// c = c0 + rel; end_r = align16(ghi) - c0 (32-bit: see process_range)
+__device__ __forceinline__ uint4 load_chunk(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r,
+                                            int lane) {
+    const uint32_t rec = end_r > rel ? min(end_r - rel, (uint32_t)kChunk) : 0u;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c0 + rel), (short)0, (int)rec, 0x00020000);
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// Tail of one lane's block; compaction shifts zeros into V above entry ne-1,
+// so ctz(~V) <= ne <= 16.
+template <int K>
+__device__ __forceinline__ uint32_t own_tail(uint32_t C, uint32_t V, uint32_t ne) {
+    constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
+    return (C & TM) | ((uint32_t)__builtin_ctz(~V) << 22) | (ne << 27);
+}
+
 // Per-lane front end shared by every path: block -> (C, V, EN, ne, own tail).
-template <int K, bool MASKED>
+template <int K, bool MASKED, bool OWN = true>
 __device__ __forceinline__ void front_end(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
                                           const ChunkMask& m, uint64_t iv0,
                                           uint32_t& C, uint32_t& V, uint32_t& EN, uint32_t& ne,
                                           uint32_t& own) {
     constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
-    uint32_t INV, NL;
-    classify16(d, C, INV, NL);
+    uint32_t INV, NNL;
+    classify16(d, C, INV, NNL);
     EN = 0xFFFFu;
     if (MASKED) apply_masks(A, chunk, lane, m, iv0, INV, EN);
     V = ~INV & 0xFFFFu;
-    ne = 16u - (uint32_t)__builtin_popcount(NL);
-    compact<MASKED>(NL, C, V, EN);
-    const uint32_t n = min((uint32_t)__builtin_ctz(~V), ne);
-    own = tail_pack(C & TM, n, ne);
+    ne = (uint32_t)__builtin_popcount(NNL);
+    compact<MASKED>(NNL ^ 0xFFFFu, C, V, EN);
+    if (OWN) own = own_tail<K>(C, V, ne);
 }
 
 // Inclusive tail of the 1 KiB chunk starting at p (warm-up only; p may lie
@@ -325,7 +334,44 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
     constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
     constexpr int W2 = 2 * K;
     uint32_t C, V, EN, ne, own;
-    front_end<K, MASKED>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
+    front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
+
+    if constexpr (ModeOf<K>::mode == kModeLds && !MASKED && ABL == 0) {
+        // Fast case (uniform, the common one): in every lane the block holds
+        // 15 or 16 entries (at most one newline), all valid, and the last k-1
+        // entries of lane L-1 (lane 0: the carry) are valid.  Then windows
+        // 0..ne-1 are valid and the context is just lane L-1's raw codes: no
+        // tails, no run mask, no inc extraction.  Test: V (zero above ne-1)
+        // must be 0x7FFF with ne == 15 or 0xFFFF with ne == 16, i.e.
+        // V ^ (ne == 16 ? 0x8000 : 0) == 0x7FFF.
+        constexpr uint32_t KM = (1u << (K - 1)) - 1u;
+        constexpr uint32_t FM = (KM << 16) | 0xFFFFu, FT = (KM << 16) | 0x7FFFu;
+        const uint32_t pC = wave_shr1(t_codes(carry), C);
+        const uint32_t pV = wave_shr1(t_n(carry) >= (uint32_t)(K - 1) ? KM : 0u, V);
+        const bool lane_ok = ((((pV << 16) | V) ^ ((ne << 11) & 0x8000u)) & FM) == FT;
+        if (__builtin_amdgcn_ballot_w64(!lane_ok) == 0) {
+            // X = (pC:C) << 2 over ne entries of C; ne in {15, 16} and C is zero
+            // above entry ne-1, so the high word is pC << (2ne+2 mod 32) | C >> 30.
+            // Byte address of window r = bits [2r, 2r+2K+2) of X, masked: 8
+            // views at bit offsets 0,2,..,14 serve r = 0..7 from their low 16
+            // bits and r = 8..15 from their high 16 bits (a word select).
+            constexpr uint32_t M4 = ((1u << W2) - 1u) << 2;
+            const uint32_t xlo = C << 2, xhi = (pC << ((2u * ne + 2u) & 31u)) | (C >> 30);
+            uint32_t xv[8];
+#pragma unroll
+            for (int o = 0; o < 8; ++o) xv[o] = o ? __builtin_amdgcn_alignbit(xhi, xlo, 2 * o) : xlo;
+            auto addr = [&](int r) -> uint32_t { return (r < 8 ? xv[r] : (xv[r - 8] >> 16)) & M4; };
+            const uint32_t inc15 = V >> 15;   // == (ne == 16)
+#pragma unroll
+            for (int r = 0; r < 15; ++r) lds_add(addr(r), 1u);
+            lds_add(addr(15), inc15);
+            lane_total += 15u + inc15;
+            // lane 63's block is all valid bases: its tail is complete
+            const uint32_t c63 = (uint32_t)__builtin_amdgcn_readlane((int)C, kWave - 1);
+            return tail_pack(c63 & TM, 31u, 31u);
+        }
+    }
+    own = own_tail<K>(C, V, ne);
 
     // context = own tail of lane L-1 (lane 0: carry), exact unless some lane is incomplete
     // A block is incomplete (needs the exact scan) only if it has fewer than k-1
@@ -337,13 +383,13 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
         if (inc_mask) ctx = scan_ctx<K>(own, carry, lane);
     }
 
-    const uint32_t ctxlen = min(t_n(ctx), (uint32_t)(K - 1));
     const uint64_t W = ((uint64_t)t_codes(ctx) << (2 * ne)) | (uint64_t)C;
+    const uint32_t wlo = (uint32_t)W, whi = (uint32_t)(W >> 32);
+    // window-validity mask R (bit r: the k-mer ending at entry r is counted)
+    const uint32_t ctxlen = min(t_n(ctx), (uint32_t)(K - 1));
     const uint32_t E = (((1u << ctxlen) - 1u) << ne) | V;
     uint32_t R = run_mask<K>(E) & ((1u << ne) - 1u);
     if (MASKED) R &= EN;
-
-    const uint32_t wlo = (uint32_t)W, whi = (uint32_t)(W >> 32);
     const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
                             __builtin_amdgcn_alignbit(whi, wlo, 24)};
     // forward window ending at entry r: bits [2r, 2r+2K) of W (first base highest)
@@ -370,22 +416,13 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
 #pragma unroll
         for (int o = 0; o < 8; ++o) xv[o] = o ? __builtin_amdgcn_alignbit(xhi, xlo, 2 * o) : xlo;
         auto addr = [&](int r) -> uint32_t { return (r < 8 ? xv[r] : (xv[r - 8] >> 16)) & M4; };
-        // Fast case (uniform): every window valid except possibly the 16th (a
-        // newline in the block leaves 15 entries) -> no per-window inc extraction.
-        const bool fast = !MASKED && __ballot((R | 0x8000u) != 0xFFFFu) == 0;
-        if (ABL == 0 && fast) {
 #pragma unroll
-            for (int r = 0; r < 15; ++r) lds_add(addr(r), 1u);
-            lds_add(addr(15), R >> 15);
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const uint32_t inc = (R >> r) & 1u;
-                if (ABL == 0)
-                    lds_add(addr(r), inc);
-                else   // profiling only (no LDS traffic)
-                    lane_total += addr(r) ^ inc;
-            }
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t inc = (R >> r) & 1u;
+            if (ABL == 0)
+                lds_add(addr(r), inc);
+            else   // profiling only (no LDS traffic)
+                lane_total += addr(r) ^ inc;
         }
     } else {
         // global path: canonical = min(fwd, revcomp) in kf code, then column via code2col
@@ -443,49 +480,60 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
         }
         iv = a;
     }
-    uint64_t iv_s = ~0ull, iv_e = ~0ull;
+    // Chunk bookkeeping in 32-bit offsets from c0 (a wave range is far below
+    // 4 GiB): gfx9 SALU has no 64-bit ordered compare, so 64-bit bounds tests
+    // would run on the VALU once per chunk.
+    const uint64_t c0 = c;
+    auto rel_of = [&](uint64_t x) -> uint32_t {
+        return x <= c0 ? 0u : (x - c0 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(x - c0));
+    };
+    uint32_t ivs_r = 0xFFFFFFFFu, ive_r = 0xFFFFFFFFu;
     if (iv < A.n_excl) {
-        iv_s = uload64(A.excl + 2 * iv);
-        iv_e = uload64(A.excl + 2 * iv + 1);
+        ivs_r = rel_of(uload64(A.excl + 2 * iv));
+        ive_r = rel_of(uload64(A.excl + 2 * iv + 1));
     }
+    const uint32_t lo_r = (uint32_t)(lo - c0), hi_r = (uint32_t)(hi - c0);
+    const uint32_t end_r = rel_of((ghi + 15) & ~(uint64_t)15);
+    uint32_t rel = 0;
     const ChunkMask m{glo, lo, hi};
     uint32_t lane_total = 0;
     // 4-deep ring, 3 chunks in flight while one is counted; a buffer is refilled
     // only after it has been consumed, so no register rotation waits on a load
-    uint4 b0 = load_chunk(A.bytes, c, ghi, lane);
-    uint4 b1 = load_chunk(A.bytes, c + kChunk, ghi, lane);
-    uint4 b2 = load_chunk(A.bytes, c + 2 * kChunk, ghi, lane);
-    uint4 b3 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+    uint4 b0 = load_chunk(A.bytes, c0, 0, end_r, lane);
+    uint4 b1 = load_chunk(A.bytes, c0, kChunk, end_r, lane);
+    uint4 b2 = load_chunk(A.bytes, c0, 2 * kChunk, end_r, lane);
+    uint4 b3 = load_chunk(A.bytes, c0, 3 * kChunk, end_r, lane);
     auto count = [&](const uint4 buf) {
-        if (c >= iv_e) {   // passed the current interval (rare)
-            do { ++iv; } while (iv < A.n_excl && uload64(A.excl + 2 * iv + 1) <= c);
-            iv_s = iv < A.n_excl ? uload64(A.excl + 2 * iv) : ~0ull;
-            iv_e = iv < A.n_excl ? uload64(A.excl + 2 * iv + 1) : ~0ull;
+        const uint64_t cc = c0 + rel;
+        if (rel >= ive_r) {   // passed the current interval (rare)
+            do { ++iv; } while (iv < A.n_excl && uload64(A.excl + 2 * iv + 1) <= cc);
+            ivs_r = iv < A.n_excl ? rel_of(uload64(A.excl + 2 * iv)) : 0xFFFFFFFFu;
+            ive_r = iv < A.n_excl ? rel_of(uload64(A.excl + 2 * iv + 1)) : 0xFFFFFFFFu;
         }
-        const bool has_iv = iv_s < c + kChunk;
-        const bool edge = c < lo || c + kChunk > hi;
+        const bool has_iv = ivs_r < rel + kChunk;
+        const bool edge = rel < lo_r || rel + kChunk > hi_r;
         if (ABL == 3) {          // profiling only: stream the bytes, no counting
             lane_total += buf.x ^ buf.y ^ buf.z ^ buf.w;
         } else if (edge || has_iv)
-            carry = count_chunk<K, true, GLOBAL, ABL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total, pass);
+            carry = count_chunk<K, true, GLOBAL, ABL>(buf, A, cc, lane, m, iv, carry, hist, gcounts, lane_total, pass);
         else
-            carry = count_chunk<K, false, GLOBAL, ABL>(buf, A, c, lane, m, iv, carry, hist, gcounts, lane_total, pass);
-        c += kChunk;
+            carry = count_chunk<K, false, GLOBAL, ABL>(buf, A, cc, lane, m, iv, carry, hist, gcounts, lane_total, pass);
+        rel += kChunk;
     };
     // steady state: groups of 4 chunks with no exit in between (keeps the
     // compiler's vmcnt bookkeeping exact: wait for the oldest load only)
-    const uint64_t nch = (hi - c + kChunk - 1) / kChunk;
-    for (uint64_t i = 0; i + 4 <= nch; i += 4) {
+    const uint32_t nch = (hi_r + kChunk - 1) / kChunk;
+    for (uint32_t i = 0; i + 4 <= nch; i += 4) {
         count(b0);
-        b0 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+        b0 = load_chunk(A.bytes, c0, rel + 3 * kChunk, end_r, lane);
         count(b1);
-        b1 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+        b1 = load_chunk(A.bytes, c0, rel + 3 * kChunk, end_r, lane);
         count(b2);
-        b2 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+        b2 = load_chunk(A.bytes, c0, rel + 3 * kChunk, end_r, lane);
         count(b3);
-        b3 = load_chunk(A.bytes, c + 3 * kChunk, ghi, lane);
+        b3 = load_chunk(A.bytes, c0, rel + 3 * kChunk, end_r, lane);
     }
-    const uint64_t rem = nch & 3;
+    const uint32_t rem = nch & 3;
     if (rem > 0) count(b0);
     if (rem > 1) count(b1);
     if (rem > 2) count(b2);
