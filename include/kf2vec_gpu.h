@@ -96,7 +96,11 @@ int kf_index_records(const uint8_t* bytes, uint64_t len, int fmt, uint64_t base,
  *   d_counts   : n_genomes x nbins uint32 (column order), zeroed first unless
  *                flags & KF_ACCUMULATE
  *   d_totals   : n_genomes uint64, number of k-mers counted per genome
- * Asynchronous on `stream`. */
+ * Asynchronous on `stream`.  For k >= 10 the library counts through a device
+ * workspace it allocates on first use (about 4.5 GB on a 256-CU device: 2 bytes
+ * of sorted records per byte of the 8 MiB genome piece each CU holds) and keeps
+ * until kf_workspace_release(); launches on different streams of one device
+ * that use it are ordered by the library. */
 int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
                    const uint64_t* d_excl, uint64_t n_excl,
                    const uint32_t* d_code2col, const uint32_t* d_col2rep, int k,
@@ -105,6 +109,10 @@ int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_gen
 /* Grid the count kernel will use on the current device for k (workgroups,
  * threads per workgroup, dynamic LDS bytes); for roofline accounting. */
 int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
+
+/* Free the large-k workspace and tables of the current device (synchronises the
+ * device).  The next large-k kf_count_batch allocates them again. */
+int kf_workspace_release(void);
 
 /* Synthetic FASTA generator on the device (benchmark/test input; spec in
  * DESIGN.md "Synthetic genomes"): genome i has id g = g0 + i*g_stride (so a rank

@@ -1,0 +1,517 @@
+// kf_bucket.hip -- canonical k-mer counting for large k (4^k bins beyond LDS).
+//
+// Reference path: kf2vec/main.py:309-323 (`jellyfish count -C -m k` + dump), the
+// same as kf_count.hip; this file serves k >= kBucketMinK, where one genome's
+// canonical bins (2,097,152 at k=11) do not fit a 160 KiB LDS and per-k-mer
+// global atomics run at ~25 G/s (measured), far below the byte stream.
+//
+// Two phases per genome piece, one workgroup (16 waves) per piece:
+//   1. scatter: each wave walks its range of the piece with the shared front end
+//      (kf_front.h); every counted window yields its canonical code in
+//      lexicographic (A0 C1 G2 T3) order, s = min(fwd, revcomp).  Rounds of
+//      16 chunks (one per wave, 16384 windows) are counting-sorted in LDS by
+//      bucket b = s >> 15 and copied out contiguously; per round the bucket
+//      offsets go to `meta`.
+//   2. count: for each bucket, the runs of that bucket from every round are
+//      histogrammed in LDS (32768 u32 = 128 KiB, index s & 0x7FFF) and flushed in
+//      column order: columns are the canonical codes in ascending order, so a
+//      bucket owns a contiguous column range [bcol[b], bcol[b+1]) and the flush
+//      writes counts with coalesced stores (col_idx[col] = s & 0x7FFF).
+// Traffic per input byte: read 1 B, write and re-read 2 B of records, plus the
+// 4 B x nbins count row per genome.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <mutex>
+#include <vector>
+
+#include "kf_front.h"
+#include "kf_internal.h"
+
+namespace kf {
+
+constexpr int kBkBits = 15;                          // 32768 codes per bucket
+constexpr uint32_t kBkCodes = 1u << kBkBits;
+constexpr int kBkWaves = 16;
+constexpr int kBkBlock = kBkWaves * kWave;
+constexpr uint32_t kRoundRecs = kBkWaves * kChunk;   // windows per round (<= 16384)
+constexpr uint64_t kPieceMax = 8ull << 20;           // bytes per piece (one workgroup)
+// rounds per piece: a wave range is <= piece/16 + 16 bytes, i.e. <= 513 chunks
+constexpr uint32_t kRmax = (uint32_t)(kPieceMax / kRoundRecs) + 2;
+constexpr uint64_t kRecCap = (uint64_t)kRmax * kRoundRecs;   // u16 records per workgroup
+
+template <int K>
+struct Bk {
+    static constexpr uint32_t nbk = (1u << (2 * K)) >> kBkBits;   // buckets
+    // LDS byte layout: histogram / round staging at 0, then counters
+    static constexpr uint32_t hist = 0;                            // 128 KiB (stage: first 32 KiB)
+    static constexpr uint32_t cnt = kBkCodes * 4;                  // nbk u32: round rank counters
+    static constexpr uint32_t rbase = cnt + nbk * 4;               // nbk+1 u32: round bucket offsets
+    static constexpr uint32_t red = (rbase + (nbk + 1) * 4 + 7) & ~7u;   // kBkWaves u64
+    static constexpr uint32_t lds_bytes = red + kBkWaves * 8;
+};
+
+struct BucketArgs {
+    const uint16_t* col_idx;   // nbins: canonical code & 0x7FFF per column
+    const uint32_t* bcol;      // nbk+1: first column of each bucket
+    const uint32_t* pstart;    // n_genomes+1: first piece of each genome
+    uint16_t* rec;             // gridDim.x * kRecCap records
+    uint16_t* meta;            // gridDim.x * (nbk+1) * kRmax round bucket offsets
+    uint32_t* roff;            // gridDim.x * kRmax round record offsets
+    uint32_t accumulate;
+};
+
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4u lds_v4u;
+
+__device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
+    return __hip_atomic_fetch_add((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_xchg(uint32_t a, uint32_t v) {
+    return __hip_atomic_exchange((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_ld(uint32_t a) { return *(volatile lds_u32*)(uintptr_t)a; }
+__device__ __forceinline__ void lds_st(uint32_t a, uint32_t v) { *(volatile lds_u32*)(uintptr_t)a = v; }
+// Barrier for LDS traffic only: outstanding global loads (the byte-stream
+// prefetch) stay in flight across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Number of pieces of a genome of `len` bytes (an empty genome still gets one:
+// its count row is written by the piece's flush).
+__device__ __forceinline__ uint32_t n_pieces(uint64_t len) {
+    return len == 0 ? 1u : (uint32_t)((len + kPieceMax - 1) / kPieceMax);
+}
+
+// pstart[g] = sum of n_pieces over genomes < g; one workgroup.
+__global__ void __launch_bounds__(1024) piece_scan_kernel(const uint64_t* goff, int32_t n, uint32_t* pstart) {
+    __shared__ uint32_t sh[1024];
+    const int t = threadIdx.x;
+    uint32_t carry = 0;
+    for (int32_t base = 0; base < n; base += 1024) {
+        const int32_t i = base + t;
+        const uint32_t v = i < n ? n_pieces(goff[i + 1] - goff[i]) : 0u;
+        sh[t] = v;
+        __syncthreads();
+        for (int d = 1; d < 1024; d <<= 1) {
+            const uint32_t o = t >= d ? sh[t - d] : 0u;
+            __syncthreads();
+            sh[t] += o;
+            __syncthreads();
+        }
+        if (i < n) pstart[i] = carry + sh[t] - v;
+        carry += sh[1023];
+        __syncthreads();
+    }
+    if (t == 0) pstart[n] = carry;
+}
+
+// Zero the count rows of genomes split into several pieces (their pieces add
+// with atomics); single-piece rows are written whole by their flush.
+__global__ void __launch_bounds__(256) zero_split_rows_kernel(const uint64_t* goff, int32_t n, uint32_t* counts,
+                                                               uint32_t nbins) {
+    for (int32_t g = blockIdx.x; g < n; g += gridDim.x) {
+        if (n_pieces(goff[g + 1] - goff[g]) <= 1) continue;
+        uint32_t* row = counts + (uint64_t)g * nbins;
+        for (uint32_t i = threadIdx.x; i < nbins; i += 256) row[i] = 0;
+    }
+}
+
+// Canonical lexicographic codes of the 16 windows of a lane (kf codes in W).
+// std code = kf ^ ((kf >> 1) & 0x55..) per base (A0 C1 T2 G3 -> A0 C1 G2 T3);
+// complement in std code = code ^ 3, so the reversed complement of the whole
+// 64-bit window register is ~revpairs, word-swapped.
+template <int K>
+__device__ __forceinline__ void canon_std(const Windows& w, uint32_t (&s)[16]) {
+    constexpr int W2 = 2 * K;
+    const uint32_t slo = w.wlo ^ ((w.wlo >> 1) & 0x55555555u);
+    const uint32_t shi = w.whi ^ ((w.whi >> 1) & 0x55555555u);
+    const uint32_t rhi = ~revpairs(slo), rlo = ~revpairs(shi);
+    constexpr int RS = 2 * (17 - K);
+    const uint32_t rplo = __builtin_amdgcn_alignbit(rhi, rlo, RS), rphi = rhi >> RS;
+    const uint32_t fv[4] = {slo, __builtin_amdgcn_alignbit(shi, slo, 8), __builtin_amdgcn_alignbit(shi, slo, 16),
+                            __builtin_amdgcn_alignbit(shi, slo, 24)};
+    const uint32_t rv[4] = {rplo, __builtin_amdgcn_alignbit(rphi, rplo, 8), __builtin_amdgcn_alignbit(rphi, rplo, 16),
+                            __builtin_amdgcn_alignbit(rphi, rplo, 24)};
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int fo = (2 * r) & ~7;
+        const uint32_t f = __builtin_amdgcn_ubfe(fv[fo >> 3], 2 * r - fo, W2);
+        const int rr = 2 * (15 - r), ro = rr & ~7;
+        const uint32_t c = __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, W2);
+        s[r] = ((w.R >> r) & 1u) ? min(f, c) : 0xFFFFFFFFu;
+    }
+}
+
+template <int K>
+__global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArgs B) {
+    using L = Bk<K>;
+    constexpr uint32_t NBK = L::nbk;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if ((uint32_t)(uintptr_t)(lds_u32*)lds != 0u) __builtin_trap();   // raw LDS addresses assume base 0
+    for (uint32_t i = tid; i < kBkCodes + NBK; i += kBkBlock) lds[i] = 0;   // histogram + counters
+    __syncthreads();
+
+    uint16_t* rec = B.rec + (uint64_t)blockIdx.x * kRecCap;
+    uint16_t* meta = B.meta + (uint64_t)blockIdx.x * (NBK + 1) * kRmax;
+    uint32_t* roff = B.roff + (uint64_t)blockIdx.x * kRmax;
+    const uint32_t npiece = B.pstart[A.n_genomes];
+
+    for (uint32_t p = blockIdx.x; p < npiece; p += gridDim.x) {
+        // genome of piece p: last g with pstart[g] <= p
+        int32_t g;
+        {
+            int32_t a = 0, e = A.n_genomes - 1;
+            while (a < e) {
+                const int32_t mid = (a + e + 1) >> 1;
+                if (B.pstart[mid] <= p) a = mid; else e = mid - 1;
+            }
+            g = a;
+        }
+        const uint32_t np = B.pstart[g + 1] - B.pstart[g], pi = p - B.pstart[g];
+        const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
+        const uint64_t plo = split_at(glo, ghi, pi, np), phi = split_at(glo, ghi, pi + 1, np);
+        const uint64_t lo = split_at(plo, phi, wave, kBkWaves), hi = split_at(plo, phi, wave + 1, kBkWaves);
+        // rounds = the longest wave range in chunks (same value in every wave)
+        uint32_t nround = 0;
+        for (int w = 0; w < kBkWaves; ++w) {
+            const uint64_t a = split_at(plo, phi, w, kBkWaves), e = split_at(plo, phi, w + 1, kBkWaves);
+            if (e > a) nround = max(nround, (uint32_t)((e - (a & ~(uint64_t)15) + kChunk - 1) / kChunk));
+        }
+
+        // ---------------------------------------------------------- phase 1
+        Range rg;
+        uint32_t nch = 0;
+        if (lo < hi) {
+            rg.begin<K>(A, glo, ghi, lo, hi, lane);
+            nch = rg.nch;
+        }
+        uint32_t carry = lo < hi ? rg.carry : 0u;
+        uint32_t off = 0;   // records written so far (multiple of 8)
+        uint32_t rel = 0;
+        uint4 buf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            buf[j] = (uint32_t)j < nch ? rg.load(A.bytes, j * kChunk, lane) : make_uint4(0u, 0u, 0u, 0u);
+        auto round = [&](uint32_t r, uint4& bf) {
+            uint32_t s[16], rk[16];
+            const bool have = r < nch;
+            if (have) {
+                Windows w;
+                uint32_t C, V, EN, ne, own;
+                if (rg.masked(A, rel)) {
+                    front_end<K, true, false>(bf, A, rg.c0 + rel, lane, rg.mask(), rg.iv, C, V, EN, ne, own);
+                    w = windows<K, true>(C, V, EN, ne, carry, lane);
+                } else {
+                    front_end<K, false, false>(bf, A, rg.c0 + rel, lane, rg.mask(), rg.iv, C, V, EN, ne, own);
+                    w = windows<K, false>(C, V, EN, ne, carry, lane);
+                }
+                carry = w.next;
+                canon_std<K>(w, s);
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (s[j] != 0xFFFFFFFFu) rk[j] = lds_add_rtn(L::cnt + ((s[j] >> kBkBits) << 2), 1u);
+                rel += kChunk;
+                if (rel + 3 * kChunk < nch * kChunk) bf = rg.load(A.bytes, rel + 3 * kChunk, lane);
+            }
+            lds_barrier();
+            // bucket offsets of this round (wave 0), counters reset for the next
+            if (wave == 0) {
+                constexpr uint32_t PER = (NBK + kWave - 1) / kWave;
+                uint32_t loc[PER];
+                uint32_t sum = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < PER; ++j) {
+                    const uint32_t b = (uint32_t)lane * PER + j;
+                    uint32_t v = 0;
+                    if (b < NBK) {
+                        v = lds_ld(L::cnt + 4 * b);
+                        lds_st(L::cnt + 4 * b, 0u);
+                    }
+                    loc[j] = sum;
+                    sum += v;
+                }
+                uint32_t inc = sum;
+#pragma unroll
+                for (int d = 1; d < kWave; d <<= 1) {
+                    const uint32_t o = __shfl_up(inc, d, kWave);
+                    if (lane >= d) inc += o;
+                }
+                const uint32_t ex = inc - sum;
+#pragma unroll
+                for (uint32_t j = 0; j < PER; ++j) {
+                    const uint32_t b = (uint32_t)lane * PER + j;
+                    if (b < NBK) {
+                        lds_st(L::rbase + 4 * b, ex + loc[j]);
+                        meta[(uint64_t)b * kRmax + r] = (uint16_t)(ex + loc[j]);
+                    }
+                }
+                if (lane == kWave - 1) {
+                    lds_st(L::rbase + 4 * NBK, inc);
+                    meta[(uint64_t)NBK * kRmax + r] = (uint16_t)inc;
+                    roff[r] = off;
+                }
+            }
+            lds_barrier();
+            if (have) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    if (s[j] != 0xFFFFFFFFu) {
+                        const uint32_t slot = lds_ld(L::rbase + ((s[j] >> kBkBits) << 2)) + rk[j];
+                        *(volatile lds_u16*)(uintptr_t)(L::hist + 2 * slot) = (uint16_t)(s[j] & (kBkCodes - 1));
+                    }
+                }
+            }
+            const uint32_t T = lds_ld(L::rbase + 4 * NBK);
+            lds_barrier();
+            // copy the sorted round out, 16 B per lane
+            for (uint32_t q = tid; q < (T + 7) / 8; q += kBkBlock) {
+                const v4u v = *(lds_v4u*)(uintptr_t)(L::hist + 16 * q);
+                *(v4u*)(rec + off + 8 * q) = v;
+            }
+            off += (T + 7) & ~7u;
+        };
+        uint32_t r = 0;
+        for (; r + 4 <= nround; r += 4) {
+            round(r, buf[0]);
+            round(r + 1, buf[1]);
+            round(r + 2, buf[2]);
+            round(r + 3, buf[3]);
+        }
+        if (r < nround) round(r++, buf[0]);
+        if (r < nround) round(r++, buf[1]);
+        if (r < nround) round(r++, buf[2]);
+
+        // ---------------------------------------------------------- phase 2
+        // records and meta were stored by other waves of this workgroup: wait for
+        // the stores, and read them with L1-bypassing loads below
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (uint32_t i = tid; i < kRoundRecs / 2; i += kBkBlock) lds_st(L::hist + 4 * i, 0u);   // staging area
+        lds_barrier();
+        uint32_t* row = A.counts + (uint64_t)g * A.nbins;
+        const bool split = np > 1;
+        unsigned long long tsum = 0;
+        // run table of this wave: lane j <-> round wave + 16 j
+        const uint32_t myr = (uint32_t)wave + kBkWaves * (uint32_t)lane;
+        const uint32_t nrun = nround > (uint32_t)wave ? (nround - (uint32_t)wave + kBkWaves - 1) / kBkWaves : 0u;
+        const uint32_t ro = myr < nround ? __builtin_nontemporal_load(roff + myr) : 0u;
+        uint32_t rs = myr < nround ? __builtin_nontemporal_load(meta + myr) : 0u;
+        for (uint32_t b = 0; b < NBK; ++b) {
+            const uint32_t re = myr < nround ? __builtin_nontemporal_load(meta + (uint64_t)(b + 1) * kRmax + myr) : 0u;
+            for (uint32_t j = 0; j < nrun; ++j) {
+                const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)rs, (int)j);
+                const uint32_t e0 = (uint32_t)__builtin_amdgcn_readlane((int)re, (int)j);
+                const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)ro, (int)j);
+                for (uint32_t q = (s0 & ~7u) + 8 * (uint32_t)lane; q < e0; q += 8 * kWave) {
+                    const v4u v = __builtin_nontemporal_load((const v4u*)(rec + base + q));
+                    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const uint32_t i = q + t;
+                        if (i >= s0 && i < e0) lds_add((((d[t >> 1] >> (16 * (t & 1))) & 0xFFFFu)) << 2, 1u);
+                    }
+                }
+            }
+            rs = re;
+            lds_barrier();
+            const uint32_t c1 = B.bcol[b + 1];
+            for (uint32_t col = B.bcol[b] + tid; col < c1; col += kBkBlock) {
+                const uint32_t v = lds_xchg((uint32_t)B.col_idx[col] << 2, 0u);
+                if (split) {
+                    if (v) __hip_atomic_fetch_add(row + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if (B.accumulate) {
+                    row[col] += v;
+                } else {
+                    row[col] = v;
+                }
+                tsum += v;
+            }
+            lds_barrier();
+        }
+        tsum = wave_sum(tsum);
+        unsigned long long* red = (unsigned long long*)((char*)lds + L::red);
+        if (lane == 0) red[wave] = tsum;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long t = 0;
+            for (int w = 0; w < kBkWaves; ++w) t += red[w];
+            if (t) atomicAdd(A.totals + g, t);
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace kf
+
+// ====================================================================== host
+using namespace kf;
+
+namespace {
+
+template <int K>
+void* bucket_ptr() { return (void*)&bucket_kernel<K>; }
+
+void* bucket_kernel_for(int k) {
+    switch (k) {
+    case 9: return bucket_ptr<9>();
+    case 10: return bucket_ptr<10>();
+    case 11: return bucket_ptr<11>();
+    case 12: return bucket_ptr<12>();
+    default: return nullptr;
+    }
+}
+uint32_t bucket_lds_for(int k) {
+    switch (k) {
+    case 9: return Bk<9>::lds_bytes;
+    case 10: return Bk<10>::lds_bytes;
+    case 11: return Bk<11>::lds_bytes;
+    case 12: return Bk<12>::lds_bytes;
+    default: return 0;
+    }
+}
+
+// Per-device state: bucket tables per k and the scratch of the last launch
+// size.  A launch on another stream waits for the previous user of the scratch.
+struct DevState {
+    uint16_t* col_idx[KF_MAX_K + 1] = {};
+    uint32_t* bcol[KF_MAX_K + 1] = {};
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    uint32_t* pstart = nullptr;
+    size_t pstart_n = 0;
+    hipEvent_t done = nullptr;
+    int grid = 0;
+};
+DevState g_dev[64];
+std::mutex g_mu;
+
+uint32_t rc_std(uint32_t s, int k) {
+    uint32_t r = 0;
+    for (int i = 0; i < k; ++i) {
+        r = (r << 2) | (3u - (s & 3u));
+        s >>= 2;
+    }
+    return r;
+}
+
+int ensure_tables(DevState& d, int k) {
+    if (d.col_idx[k]) return KF_OK;
+    const uint32_t ncode = 1u << (2 * k), nbk = ncode >> kBkBits;
+    std::vector<uint16_t> ci;
+    std::vector<uint32_t> bc(nbk + 1, 0);
+    ci.reserve(kf_num_bins(k));
+    for (uint32_t s = 0; s < ncode; ++s) {
+        if ((s & (kBkCodes - 1)) == 0) bc[s >> kBkBits] = (uint32_t)ci.size();
+        if (s <= rc_std(s, k)) ci.push_back((uint16_t)(s & (kBkCodes - 1)));
+    }
+    bc[nbk] = (uint32_t)ci.size();
+    if (ci.size() != kf_num_bins(k)) return kf_fail(KF_EINVAL, "bucket table: %zu canonical codes", ci.size());
+    if (hipMalloc((void**)&d.col_idx[k], ci.size() * 2) != hipSuccess ||
+        hipMalloc((void**)&d.bcol[k], bc.size() * 4) != hipSuccess)
+        return kf_fail(KF_EHIP, "hipMalloc of bucket tables failed");
+    if (hipMemcpy(d.col_idx[k], ci.data(), ci.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d.bcol[k], bc.data(), bc.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return kf_fail(KF_EHIP, "hipMemcpy of bucket tables failed");
+    return KF_OK;
+}
+
+}  // namespace
+
+namespace kf {
+
+int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
+    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
+    void* fn = bucket_kernel_for(k);
+    if (!fn) return kf_fail(KF_EINVAL, "no bucket kernel for k=%d", k);
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevState& d = g_dev[dev];
+    int rc = ensure_tables(d, k);
+    if (rc) return rc;
+    const uint32_t lds = bucket_lds_for(k), nbk = (1u << (2 * k)) >> kBkBits;
+    if (!d.grid) {
+        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipDeviceGetAttribute(MultiprocessorCount) failed");
+        d.grid = cus > 0 ? cus : 1;
+        if (hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipEventCreate failed");
+    } else if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+        return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    }
+    const int grid = d.grid;
+    // scratch: records, round metadata (sized for the largest k), round offsets
+    const size_t rec_b = (size_t)grid * kRecCap * 2;
+    const size_t meta_b = (size_t)grid * (((1u << (2 * KF_MAX_K)) >> kBkBits) + 1) * kRmax * 2;
+    const size_t roff_b = (size_t)grid * kRmax * 4;
+    const size_t need = rec_b + meta_b + roff_b;
+    if (d.done && hipStreamWaitEvent(s, d.done, 0) != hipSuccess)
+        return kf_fail(KF_EHIP, "hipStreamWaitEvent failed");
+    if (d.scratch_bytes < need) {
+        if (d.scratch && (hipDeviceSynchronize() != hipSuccess || hipFree(d.scratch) != hipSuccess))
+            return kf_fail(KF_EHIP, "hipFree of bucket scratch failed");
+        d.scratch = nullptr;
+        d.scratch_bytes = 0;
+        if (hipMalloc(&d.scratch, need) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipMalloc of %zu bytes of bucket scratch failed", need);
+        d.scratch_bytes = need;
+    }
+    if (d.pstart_n < (size_t)A.n_genomes + 1) {
+        if (d.pstart && (hipDeviceSynchronize() != hipSuccess || hipFree(d.pstart) != hipSuccess))
+            return kf_fail(KF_EHIP, "hipFree of piece table failed");
+        d.pstart = nullptr;
+        d.pstart_n = 0;
+        if (hipMalloc((void**)&d.pstart, ((size_t)A.n_genomes + 1) * 4) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipMalloc of piece table failed");
+        d.pstart_n = (size_t)A.n_genomes + 1;
+    }
+    BucketArgs B;
+    B.col_idx = d.col_idx[k];
+    B.bcol = d.bcol[k];
+    B.pstart = d.pstart;
+    B.rec = (uint16_t*)d.scratch;
+    B.meta = (uint16_t*)((char*)d.scratch + rec_b);
+    B.roff = (uint32_t*)((char*)d.scratch + rec_b + meta_b);
+    B.accumulate = (flags & KF_ACCUMULATE) ? 1u : 0u;
+    (void)nbk;
+    hipLaunchKernelGGL(piece_scan_kernel, dim3(1), dim3(1024), 0, s, A.goff, A.n_genomes, d.pstart);
+    if (!B.accumulate)
+        hipLaunchKernelGGL(zero_split_rows_kernel, dim3(1024), dim3(256), 0, s, A.goff, A.n_genomes, A.counts,
+                           A.nbins);
+    void* args[] = {(void*)&A, (void*)&B};
+    if (hipLaunchKernel(fn, dim3(grid), dim3(kBkBlock), args, lds, s) != hipSuccess)
+        return kf_fail(KF_EHIP, "bucket kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (hipEventRecord(d.done, s) != hipSuccess) return kf_fail(KF_EHIP, "hipEventRecord failed");
+    return KF_OK;
+}
+
+}  // namespace kf
+
+extern "C" int kf_workspace_release(void) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
+    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevState& d = g_dev[dev];
+    if (hipDeviceSynchronize() != hipSuccess) return kf_fail(KF_EHIP, "hipDeviceSynchronize failed");
+    for (int k = 0; k <= KF_MAX_K; ++k) {
+        if (d.col_idx[k]) (void)hipFree(d.col_idx[k]);
+        if (d.bcol[k]) (void)hipFree(d.bcol[k]);
+        d.col_idx[k] = nullptr;
+        d.bcol[k] = nullptr;
+    }
+    if (d.scratch) (void)hipFree(d.scratch);
+    if (d.pstart) (void)hipFree(d.pstart);
+    d.scratch = nullptr;
+    d.scratch_bytes = 0;
+    d.pstart = nullptr;
+    d.pstart_n = 0;
+    return KF_OK;
+}

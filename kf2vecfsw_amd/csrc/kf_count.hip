@@ -25,12 +25,11 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "kf_front.h"
 #include "kf_internal.h"
 
 namespace kf {
 
-constexpr int kWave = 64;
-constexpr int kChunk = 1024;       // bytes per wave iteration (64 lanes x 16 B)
 // Workgroup shapes ("variants"): one 4^k-entry LDS histogram is shared by all
 // waves of a workgroup, so a bigger workgroup raises occupancy at equal LDS.
 //   variant 0: 512 threads (8 waves), 2 workgroups/CU at k=7
@@ -58,6 +57,7 @@ template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 
 constexpr int kLdsMaxK = 7;
 constexpr int kMultiMaxK = 9;
 constexpr int kMultiBits = 15;
+constexpr int kDefaultBucketMinK = 10;
 enum { kModeLds = 0, kModeMulti = 1, kModeGlobal = 2 };
 template <int K>
 struct ModeOf {
@@ -67,263 +67,6 @@ struct ModeOf {
                                         : (mode == kModeMulti ? (1u << kMultiBits) : 0u);
 };
 
-struct CountArgs {
-    const uint8_t* bytes;
-    const uint64_t* goff;
-    const uint64_t* excl;          // [s0,e0,s1,e1,...]
-    uint64_t n_excl;
-    const uint32_t* code2col;
-    const uint32_t* col2rep;
-    uint32_t* counts;
-    unsigned long long* totals;
-    uint32_t nbins;
-    int32_t n_genomes;
-};
-
-// ---------------------------------------------------------------- tails
-// A "tail" summarises a stretch of the compacted entry stream:
-//   codes [0,22): the last <= k-1 entries' 2-bit codes (last entry lowest)
-//   n     [22,27): length of the trailing run of valid bases (capped at 31)
-//   ne    [27,32): number of entries (capped at 31)
-__device__ __forceinline__ uint32_t tail_pack(uint32_t codes, uint32_t n, uint32_t ne) {
-    return codes | (min(n, 31u) << 22) | (min(ne, 31u) << 27);
-}
-__device__ __forceinline__ uint32_t t_codes(uint32_t t) { return t & 0x3FFFFFu; }
-__device__ __forceinline__ uint32_t t_n(uint32_t t) { return (t >> 22) & 31u; }
-__device__ __forceinline__ uint32_t t_ne(uint32_t t) { return t >> 27; }
-
-template <int K>
-__device__ __forceinline__ uint32_t tail_combine(uint32_t a, uint32_t b) {
-    constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
-    const uint32_t bn = t_n(b), bne = t_ne(b);
-    const uint32_t n = (bn < bne) ? bn : min(t_n(a) + bn, 31u);
-    const uint32_t codes =
-        (bne >= (uint32_t)(K - 1)) ? t_codes(b) : (((t_codes(a) << (2 * bne)) | t_codes(b)) & TM);
-    return tail_pack(codes, n, t_ne(a) + bne);
-}
-template <int K>
-__device__ __forceinline__ bool tail_complete(uint32_t t) {
-    return t_n(t) < t_ne(t) || t_n(t) >= (uint32_t)(K - 1);
-}
-
-// ---------------------------------------------------------------- classify
-// 16 bytes -> codes C (byte i at bits 2(15-i)), invalid mask INV and
-// not-newline mask NNL (byte i at bit 15-i).  Valid bases: ACGTacgt.
-//   cb = (b >> 1) & 3            kf code (A0 C1 T2 G3)
-//   y  = (b ^ TBL[cb]) & 0xDF    == 0x0C iff b is the base cb (either case)
-//   perm(-1,-1,sel) yields 0x00 for sel == 12 and 0xFF for every other byte
-//   dot4 packs four codes / four flags into one byte / nibble in memory order.
-__device__ __forceinline__ void classify16(const uint4 d, uint32_t& C, uint32_t& INV, uint32_t& NNL) {
-    const uint32_t w[4] = {d.x, d.y, d.z, d.w};
-    uint32_t pc[4], vf[4], nf[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t x = w[q];
-        const uint32_t cb = (x >> 1) & 0x03030303u;
-        const uint32_t ex = __builtin_amdgcn_perm(0u, 0x4B584F4Du, cb);   // "ACTG" ^ 0x0C
-        const uint32_t y = (x ^ ex) & 0xDFDFDFDFu;
-        vf[q] = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, y);          // 0x00 valid base
-        nf[q] = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, x ^ 0x06060606u);   // 0x00 newline
-        pc[q] = __builtin_amdgcn_udot4(cb, 0x01041040u, 0u, false);
-    }
-    // codes: byte q of C (from the top) = pc[q]
-    const uint32_t c01 = __builtin_amdgcn_perm(pc[0], pc[1], 0x0C0C0400u);
-    const uint32_t c23 = __builtin_amdgcn_perm(pc[2], pc[3], 0x0C0C0400u);
-    C = (c01 << 16) | c23;
-    // flag bytes are 0x00 / 0xFF (= -1 signed).  Weights -8,-4,-2,-1 give dword
-    // q+1's nibble and -128,-64,-32,-16 dword q's nibble one position up, so one
-    // accumulating dot pair packs a byte of the mask.
-    auto pair = [](const uint32_t a, const uint32_t b) -> uint32_t {
-        return (uint32_t)__builtin_amdgcn_sdot4((int)a, (int)0xF0E0C080u,
-                                               __builtin_amdgcn_sdot4((int)b, (int)0xFFFEFCF8u, 0, false), false);
-    };
-    INV = (pair(vf[0], vf[1]) << 8) | pair(vf[2], vf[3]);
-    NNL = (pair(nf[0], nf[1]) << 8) | pair(nf[2], nf[3]);   // not-newline mask
-}
-
-// Remove newline entries (compaction).  C: 2-bit entries, V/EN: 1-bit masks,
-// entry r at bits [2r, 2r+2) / bit r.  The lowest newline is removed branch-free
-// (r = 16 sentinel when there is none: every mask becomes the identity); any
-// further newline in the same 16 bytes (lines shorter than 16) takes the loop.
-__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
-
-template <bool MASKED>
-__device__ __forceinline__ void remove_entry(uint32_t r, uint32_t& C, uint32_t& V, uint32_t& EN, uint32_t& nl) {
-    const uint32_t lo1 = (1u << r) - 1u;          // entries below r stay
-    const uint32_t lo2 = lo1 | (lo1 << r);         // (1 << 2r) - 1, also for r = 16
-    V = bfi(lo1, V, V >> 1);
-    if (MASKED) EN = bfi(lo1, EN, EN >> 1);
-    C = bfi(lo2, C, C >> 2);
-    nl = (nl >> 1) & ~lo1;                         // drop bit r, shift the rest down
-}
-
-template <bool MASKED>
-__device__ __forceinline__ void compact(uint32_t nl, uint32_t& C, uint32_t& V, uint32_t& EN) {
-    remove_entry<MASKED>((uint32_t)__builtin_ctz(nl | 0x10000u), C, V, EN, nl);
-    while (nl) remove_entry<MASKED>((uint32_t)__builtin_ctz(nl), C, V, EN, nl);
-}
-
-__device__ __forceinline__ uint32_t revpairs(uint32_t x) {
-    const uint32_t t = __builtin_bitreverse32(x);
-    return ((t << 1) & 0xAAAAAAAAu) | ((t >> 1) & 0x55555555u);
-}
-
-// reverse complement of a K-mer in kf code (complement = code ^ 2)
-template <int K>
-__device__ __forceinline__ uint32_t kf_revcomp(uint32_t x) {
-    return (revpairs(x) >> (32 - 2 * K)) ^ (0xAAAAAAAAu >> (32 - 2 * K));
-}
-
-template <int K>
-__device__ __forceinline__ uint32_t run_mask(uint32_t E) {
-    // bit r set iff entries r .. r+K-1 are all valid
-    uint32_t R = E;
-    int a = 1;
-#pragma unroll
-    for (int it = 0; it < 5; ++it) {
-        if (a < K) {
-            const int s = (a < K - a) ? a : (K - a);
-            R &= R >> s;
-            a += s;
-        }
-    }
-    return R;
-}
-
-// Atomic add to the LDS word at byte address `a`.  The histogram is the whole
-// dynamic LDS allocation and the kernel declares no static LDS, so it starts at
-// LDS address 0 (checked once per kernel): a raw address-space-3 pointer avoids a
-// base add per k-mer.
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-__device__ __forceinline__ void lds_add(uint32_t a, uint32_t v) {
-    __hip_atomic_fetch_add((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ uint32_t wave_shr1(uint32_t old, uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
-}
-
-// Exclusive scan of lane tails with a carry-in (slow path: some lane's block has
-// fewer than k-1 entries and no reset, e.g. very short FASTA lines).
-template <int K>
-__device__ __noinline__ uint32_t scan_ctx(uint32_t own, uint32_t carry, int lane) {
-    uint32_t v = own;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t o = __shfl_up(v, d, kWave);
-        if (lane >= d) v = tail_combine<K>(o, v);
-    }
-    const uint32_t ex = __shfl_up(v, 1, kWave);
-    return lane == 0 ? carry : tail_combine<K>(carry, ex);
-}
-
-// Load a wave-uniform 64-bit word and pin it in SGPRs: compares against it then
-// never wait on the vector-memory counter shared with the byte-stream prefetch.
-__device__ __forceinline__ uint64_t uload64(const uint64_t* p) {
-    const uint64_t v = *p;
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-}
-
-struct ChunkMask {
-    // byte-position bounds for masked chunks (absolute offsets)
-    uint64_t glo;   // bytes < glo are invalid (previous genome)
-    uint64_t lo;    // count only windows ending at bytes in [lo, hi)
-    uint64_t hi;
-};
-
-__device__ __forceinline__ uint32_t range_bits(int64_t a, int64_t b) {
-    // bits for bytes [a, b) of a 16-byte block (byte i at bit 15-i), a,b clamped to [0,16]
-    a = a < 0 ? 0 : (a > 16 ? 16 : a);
-    b = b < 0 ? 0 : (b > 16 ? 16 : b);
-    if (b <= a) return 0u;
-    const uint32_t n = (uint32_t)(b - a);
-    return ((n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << (16 - (uint32_t)b)) & 0xFFFFu;
-}
-
-// Apply genome start / count window / excluded intervals to one lane's block.
-__device__ __forceinline__ void apply_masks(const CountArgs& A, uint64_t chunk, int lane,
-                                            const ChunkMask& m, uint64_t iv0,
-                                            uint32_t& INV, uint32_t& EN) {
-    const int64_t b0 = (int64_t)(chunk + 16u * (uint32_t)lane);
-    INV |= range_bits(-1, (int64_t)m.glo - b0);
-    EN = range_bits((int64_t)m.lo - b0, (int64_t)m.hi - b0);
-    const uint64_t cend = chunk + kChunk;
-    for (uint64_t i = iv0; i < A.n_excl; ++i) {      // wave-uniform loop
-        const uint64_t s = uload64(A.excl + 2 * i), e = uload64(A.excl + 2 * i + 1);
-        if (s >= cend) break;
-        INV |= range_bits((int64_t)s - b0, (int64_t)e - b0);
-    }
-}
-
-// Buffer descriptor of the chunk at c, clamped to the genome end rounded up to
-// 16 bytes: the hardware range check zeroes a whole dword/vector that straddles
-// num_records, so an exact (unaligned) end would drop the genome's last bases.
-// Bytes in [ghi, align16(ghi)) are read but never counted (they lie past hi).
-// c = c0 + rel; end_r = align16(ghi) - c0 (32-bit: see process_range)
-__device__ __forceinline__ uint4 load_chunk(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r,
-                                            int lane) {
-    const uint32_t rec = end_r > rel ? min(end_r - rel, (uint32_t)kChunk) : 0u;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c0 + rel), (short)0, (int)rec, 0x00020000);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-
-// Tail of one lane's block; compaction shifts zeros into V above entry ne-1,
-// so ctz(~V) <= ne <= 16.
-template <int K>
-__device__ __forceinline__ uint32_t own_tail(uint32_t C, uint32_t V, uint32_t ne) {
-    constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
-    return (C & TM) | ((uint32_t)__builtin_ctz(~V) << 22) | (ne << 27);
-}
-
-// Per-lane front end shared by every path: block -> (C, V, EN, ne, own tail).
-template <int K, bool MASKED, bool OWN = true>
-__device__ __forceinline__ void front_end(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
-                                          const ChunkMask& m, uint64_t iv0,
-                                          uint32_t& C, uint32_t& V, uint32_t& EN, uint32_t& ne,
-                                          uint32_t& own) {
-    constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
-    uint32_t INV, NNL;
-    classify16(d, C, INV, NNL);
-    EN = 0xFFFFu;
-    if (MASKED) apply_masks(A, chunk, lane, m, iv0, INV, EN);
-    V = ~INV & 0xFFFFu;
-    ne = (uint32_t)__builtin_popcount(NNL);
-    compact<MASKED>(NNL ^ 0xFFFFu, C, V, EN);
-    if (OWN) own = own_tail<K>(C, V, ne);
-}
-
-// Inclusive tail of the 1 KiB chunk starting at p (warm-up only; p may lie
-// before glo or even before the buffer: those bytes read as invalid).
-template <int K>
-__device__ __noinline__ uint32_t chunk_tail(const uint8_t* bytes, const uint64_t* excl, uint64_t n_excl, int64_t p,
-                                            uint64_t glo, int lane) {
-    CountArgs A{};
-    A.bytes = bytes;
-    A.excl = excl;
-    A.n_excl = n_excl;
-    const int64_t b0 = p + 16 * lane;
-    uint4 d = make_uint4(0u, 0u, 0u, 0u);
-    if (b0 >= (int64_t)(glo & ~(uint64_t)15)) d = *(const uint4*)(A.bytes + b0);
-    // first excluded interval that ends after the chunk start (binary search)
-    const uint64_t key = p < 0 ? 0 : (uint64_t)p;
-    uint64_t lo = 0, hi = A.n_excl;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (A.excl[2 * mid + 1] <= key) lo = mid + 1; else hi = mid;
-    }
-    ChunkMask m{glo, 0, 0};
-    uint32_t C, V, EN, ne, own;
-    front_end<K, true>(d, A, (uint64_t)p, lane, m, lo, C, V, EN, ne, own);
-    uint32_t v = own;
-#pragma unroll
-    for (int dd = 1; dd < kWave; dd <<= 1) {
-        const uint32_t o = __shfl_up(v, dd, kWave);
-        if (lane >= dd) v = tail_combine<K>(o, v);
-    }
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, kWave - 1);
-}
 
 // Count one chunk.  GLOBAL = count straight into d_counts (k > kLdsMaxK).
 template <int K, bool MASKED, bool GLOBAL, int ABL>
@@ -371,25 +114,8 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
             return tail_pack(c63 & TM, 31u, 31u);
         }
     }
-    own = own_tail<K>(C, V, ne);
-
-    // context = own tail of lane L-1 (lane 0: carry), exact unless some lane is incomplete
-    // A block is incomplete (needs the exact scan) only if it has fewer than k-1
-    // entries and no reset; ne < k-1 needs >= 17-k newlines in 16 bytes, so test
-    // that first (one compare) and refine only when it fires.
-    uint32_t ctx = wave_shr1(carry, own);
-    if (__ballot(ne < (uint32_t)(K - 1)) != 0) {
-        const uint64_t inc_mask = __ballot(!tail_complete<K>(own)) & 0x7FFFFFFFFFFFFFFFull;
-        if (inc_mask) ctx = scan_ctx<K>(own, carry, lane);
-    }
-
-    const uint64_t W = ((uint64_t)t_codes(ctx) << (2 * ne)) | (uint64_t)C;
-    const uint32_t wlo = (uint32_t)W, whi = (uint32_t)(W >> 32);
-    // window-validity mask R (bit r: the k-mer ending at entry r is counted)
-    const uint32_t ctxlen = min(t_n(ctx), (uint32_t)(K - 1));
-    const uint32_t E = (((1u << ctxlen) - 1u) << ne) | V;
-    uint32_t R = run_mask<K>(E) & ((1u << ne) - 1u);
-    if (MASKED) R &= EN;
+    const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
+    const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
     const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
                             __builtin_amdgcn_alignbit(whi, wlo, 24)};
     // forward window ending at entry r: bits [2r, 2r+2K) of W (first base highest)
@@ -445,9 +171,7 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
         }
     }
     lane_total += (uint32_t)__builtin_popcount(R);
-    // inclusive tail of lane 63 = next chunk's carry
-    const uint32_t incl = tail_pack(wlo & TM, (uint32_t)__builtin_ctz(~E), 31u);
-    return (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    return win.next;
 }
 
 // Process the wave range [lo, hi) of genome [glo, ghi).
@@ -455,83 +179,43 @@ template <int K, bool GLOBAL, int ABL>
 __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                   uint64_t lo, uint64_t hi, int lane,
                                                   uint32_t* __restrict__ hist, uint32_t pass) {
-    uint64_t c = lo & ~(uint64_t)15;
     if (lo >= hi) return 0;
     uint32_t* gcounts = GLOBAL ? A.counts + (uint64_t)g * A.nbins : nullptr;
-
-    // warm-up: exact k-1 context before c (walk back until complete)
-    uint32_t carry = tail_pack(0, 0, 0);
-    {
-        int64_t p = (int64_t)c;
-        while (p > (int64_t)glo && !tail_complete<K>(carry)) {
-            p -= kChunk;
-            carry = tail_combine<K>(chunk_tail<K>(A.bytes, A.excl, A.n_excl, p, glo, lane), carry);
-        }
-    }
-    // first excluded interval ending after c; its bounds live in registers so the
-    // chunk loop issues no vector loads besides the byte stream (a VMEM load there
-    // would force vmcnt(0) and drain the prefetch ring)
-    uint64_t iv = 0;
-    {
-        uint64_t a = 0, b = A.n_excl;
-        while (a < b) {
-            const uint64_t mid = (a + b) >> 1;
-            if (uload64(A.excl + 2 * mid + 1) <= c) a = mid + 1; else b = mid;
-        }
-        iv = a;
-    }
-    // Chunk bookkeeping in 32-bit offsets from c0 (a wave range is far below
-    // 4 GiB): gfx9 SALU has no 64-bit ordered compare, so 64-bit bounds tests
-    // would run on the VALU once per chunk.
-    const uint64_t c0 = c;
-    auto rel_of = [&](uint64_t x) -> uint32_t {
-        return x <= c0 ? 0u : (x - c0 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(x - c0));
-    };
-    uint32_t ivs_r = 0xFFFFFFFFu, ive_r = 0xFFFFFFFFu;
-    if (iv < A.n_excl) {
-        ivs_r = rel_of(uload64(A.excl + 2 * iv));
-        ive_r = rel_of(uload64(A.excl + 2 * iv + 1));
-    }
-    const uint32_t lo_r = (uint32_t)(lo - c0), hi_r = (uint32_t)(hi - c0);
-    const uint32_t end_r = rel_of((ghi + 15) & ~(uint64_t)15);
+    Range rg;
+    rg.begin<K>(A, glo, ghi, lo, hi, lane);
+    uint32_t carry = rg.carry;
     uint32_t rel = 0;
-    const ChunkMask m{glo, lo, hi};
+    const ChunkMask m = rg.mask();
     uint32_t lane_total = 0;
     // 4-deep ring, 3 chunks in flight while one is counted; a buffer is refilled
     // only after it has been consumed, so no register rotation waits on a load
-    uint4 b0 = load_chunk(A.bytes, c0, 0, end_r, lane);
-    uint4 b1 = load_chunk(A.bytes, c0, kChunk, end_r, lane);
-    uint4 b2 = load_chunk(A.bytes, c0, 2 * kChunk, end_r, lane);
-    uint4 b3 = load_chunk(A.bytes, c0, 3 * kChunk, end_r, lane);
+    uint4 b0 = rg.load(A.bytes, 0, lane);
+    uint4 b1 = rg.load(A.bytes, kChunk, lane);
+    uint4 b2 = rg.load(A.bytes, 2 * kChunk, lane);
+    uint4 b3 = rg.load(A.bytes, 3 * kChunk, lane);
     auto count = [&](const uint4 buf) {
-        const uint64_t cc = c0 + rel;
-        if (rel >= ive_r) {   // passed the current interval (rare)
-            do { ++iv; } while (iv < A.n_excl && uload64(A.excl + 2 * iv + 1) <= cc);
-            ivs_r = iv < A.n_excl ? rel_of(uload64(A.excl + 2 * iv)) : 0xFFFFFFFFu;
-            ive_r = iv < A.n_excl ? rel_of(uload64(A.excl + 2 * iv + 1)) : 0xFFFFFFFFu;
-        }
-        const bool has_iv = ivs_r < rel + kChunk;
-        const bool edge = rel < lo_r || rel + kChunk > hi_r;
+        const uint64_t cc = rg.c0 + rel;
+        const bool msk = rg.masked(A, rel);
         if (ABL == 3) {          // profiling only: stream the bytes, no counting
             lane_total += buf.x ^ buf.y ^ buf.z ^ buf.w;
-        } else if (edge || has_iv)
-            carry = count_chunk<K, true, GLOBAL, ABL>(buf, A, cc, lane, m, iv, carry, hist, gcounts, lane_total, pass);
+        } else if (msk)
+            carry = count_chunk<K, true, GLOBAL, ABL>(buf, A, cc, lane, m, rg.iv, carry, hist, gcounts, lane_total, pass);
         else
-            carry = count_chunk<K, false, GLOBAL, ABL>(buf, A, cc, lane, m, iv, carry, hist, gcounts, lane_total, pass);
+            carry = count_chunk<K, false, GLOBAL, ABL>(buf, A, cc, lane, m, rg.iv, carry, hist, gcounts, lane_total, pass);
         rel += kChunk;
     };
     // steady state: groups of 4 chunks with no exit in between (keeps the
     // compiler's vmcnt bookkeeping exact: wait for the oldest load only)
-    const uint32_t nch = (hi_r + kChunk - 1) / kChunk;
+    const uint32_t nch = rg.nch;
     for (uint32_t i = 0; i + 4 <= nch; i += 4) {
         count(b0);
-        b0 = load_chunk(A.bytes, c0, rel + 3 * kChunk, end_r, lane);
+        b0 = rg.load(A.bytes, rel + 3 * kChunk, lane);
         count(b1);
-        b1 = load_chunk(A.bytes, c0, rel + 3 * kChunk, end_r, lane);
+        b1 = rg.load(A.bytes, rel + 3 * kChunk, lane);
         count(b2);
-        b2 = load_chunk(A.bytes, c0, rel + 3 * kChunk, end_r, lane);
+        b2 = rg.load(A.bytes, rel + 3 * kChunk, lane);
         count(b3);
-        b3 = load_chunk(A.bytes, c0, rel + 3 * kChunk, end_r, lane);
+        b3 = rg.load(A.bytes, rel + 3 * kChunk, lane);
     }
     const uint32_t rem = nch & 3;
     if (rem > 0) count(b0);
@@ -540,11 +224,6 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
     return lane_total;
 }
 
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, kWave);
-    return v;
-}
 
 template <int K, int V>
 __global__ void __launch_bounds__(Shape<V>::block)
@@ -591,14 +270,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
         const uint64_t plo = max(glo, span_lo), phi = min(ghi, span_hi);
         if (phi <= plo) continue;
         // wave w owns [split(w), split(w+1)): 16-byte aligned, monotone, covering [plo, phi)
-        const uint64_t len = phi - plo;
-        auto split = [&](uint64_t w) -> uint64_t {
-            if (w == 0) return plo;
-            if (w >= (uint64_t)kWaves) return phi;
-            const uint64_t s = (plo + len / kWaves * w + (len % kWaves) * w / kWaves) & ~(uint64_t)15;
-            return min(max(s, plo), phi);
-        };
-        const uint64_t lo_c = split(wave), hi_c = split(wave + 1);
+        const uint64_t lo_c = split_at(plo, phi, wave, kWaves), hi_c = split_at(plo, phi, wave + 1, kWaves);
         if (GLOBAL) {
             const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
             const unsigned long long s = wave_sum(lt);
@@ -761,6 +433,16 @@ void* count_kernel_for(int k, int v) {
 }
 int block_for(int v) { return v == 0 ? Shape<0>::block : Shape<1>::block; }
 
+// KF_BUCKET_MIN_K (A-B knob, read per launch): smallest k counted by the bucket
+// kernels (kf_bucket.hip); below it k 8..9 use multi-pass LDS and k >= 10 global
+// atomics.
+int bucket_min_k() {
+    const char* e = getenv("KF_BUCKET_MIN_K");
+    if (!e || !*e) return kDefaultBucketMinK;
+    const int v = atoi(e);
+    return (v >= 9 && v <= KF_MAX_K + 1) ? v : kDefaultBucketMinK;
+}
+
 // KF_COUNT_VARIANT (tuning/A-B knob, read per launch): workgroup shape, see Shape<>.
 int current_variant() {
     const char* e = getenv("KF_COUNT_VARIANT");
@@ -830,14 +512,12 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     if (((uintptr_t)d_bytes) & 15) return kf_fail(KF_EINVAL, "d_bytes must be 16-byte aligned");
     const uint64_t nb = kf_num_bins(k);
     hipStream_t s = (hipStream_t)stream;
+    const bool bucket = k >= bucket_min_k();
     if (!(flags & KF_ACCUMULATE)) {
-        if (hipMemsetAsync(d_counts, 0, (size_t)n_genomes * nb * sizeof(uint32_t), s) != hipSuccess ||
+        if ((!bucket && hipMemsetAsync(d_counts, 0, (size_t)n_genomes * nb * sizeof(uint32_t), s) != hipSuccess) ||
             hipMemsetAsync(d_totals, 0, (size_t)n_genomes * sizeof(uint64_t), s) != hipSuccess)
             return kf_fail(KF_EHIP, "hipMemsetAsync failed");
     }
-    int grid = 0, block = 0, lds = 0, variant = 0;
-    int rc = launch_info(k, &grid, &block, &lds, &variant);
-    if (rc) return rc;
     CountArgs A;
     A.bytes = d_bytes;
     A.goff = d_goff;
@@ -849,6 +529,10 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.totals = (unsigned long long*)d_totals;
     A.nbins = (uint32_t)nb;
     A.n_genomes = n_genomes;
+    if (bucket) return bucket_launch(A, k, flags, s);
+    int grid = 0, block = 0, lds = 0, variant = 0;
+    int rc = launch_info(k, &grid, &block, &lds, &variant);
+    if (rc) return rc;
     void* args[] = {&A};
     if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));

@@ -7,3 +7,4 @@
 
 // Records the thread-local error message and returns `code`.
 int kf_fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+

@@ -136,7 +136,7 @@ def test_one_large_genome_split_across_all_workgroups(torch_dev, oracle):
     rng = np.random.default_rng(9)
     seq = gen.random_seq(rng, 60_000_000, n_rate=1e-5, lower=0.01)
     blob = b">big\n" + gen.wrap(seq, 61)
-    for k in (7, 9):
+    for k in (7, 9, 11):    # k=11: 8 bucket-kernel pieces adding into one row
         counts, totals = run_batch([blob], k, torch_dev)
         check_against_oracle(oracle, [blob], k, counts, totals, tag="big")
 
@@ -169,11 +169,12 @@ def test_device_synth_matches_oracle_and_counts(torch_dev, oracle):
                 assert t == L - 7 + 1
 
 
-def test_deterministic_and_accumulate(torch_dev, oracle):
+@pytest.mark.parametrize("k", [7, 11])
+def test_deterministic_and_accumulate(torch_dev, oracle, k):
     import torch
     from kf2vecfsw_amd import counter as C
     db = C.synth_device_batch(16, 1_000_000, seed0=1, device=torch_dev)
-    kc = counter(7, torch_dev)
+    kc = counter(k, torch_dev)
     a, ta = kc.count(db)
     a = a.clone()
     b, tb = kc.count(db)
@@ -246,3 +247,43 @@ def test_cli_get_kmers_matches_oracle(torch_dev, toy, oracle, tmp_path):
         c, _ = oracle.count(data, 7)
         ref = oracle.kmers_matrix_from_dump(oracle.dump_lines(c, 7), 7)
         assert m.dtype == np.float32 and np.array_equal(m, ref), sample
+
+
+@pytest.mark.parametrize("k", [10, 12])
+def test_bucket_mixed_batch_and_accumulate(torch_dev, oracle, k):
+    """Large-k bucket kernels: empty and tiny genomes, one genome split into 3
+    pieces (> 8 MiB: atomic flush into a pre-zeroed row), accumulate on top."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    rng = np.random.default_rng(40 + k)
+    big = b">big\n" + gen.wrap(gen.random_seq(rng, 20_000_000, n_rate=1e-5), 70)
+    blobs = [b"", b">t\nACGTACGTACGTA\n", big, b">e\n"] + \
+        [gen.random_fasta(rng, int(rng.integers(0, 300000)), max_records=4, n_rate=0.001, lower=0.05)
+         for _ in range(12)]
+    hb = C.pack_genomes(blobs)
+    db = C.to_device(hb, torch_dev)
+    kc = counter(k, torch_dev)
+    cnt, tot = kc.count(db)
+    torch.cuda.synchronize()
+    counts, totals = C.counts_to_numpy(cnt), tot.cpu().numpy()
+    check_against_oracle(oracle, blobs, k, counts, totals, tag="bucket")
+    kc.count(db, cnt, tot, accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(C.counts_to_numpy(cnt), 2 * counts)
+    assert np.array_equal(tot.cpu().numpy(), 2 * totals)
+
+
+@pytest.mark.parametrize("k", [9, 10])
+def test_bucket_kernel_agrees_with_other_large_k_paths(torch_dev, monkeypatch, k):
+    """k=9: bucket vs multi-pass LDS; k=10: bucket vs global atomics (KF_BUCKET_MIN_K)."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    db = C.synth_device_batch(40, 700_000, seed0=5, n_period=3, device=torch_dev)
+    kc = counter(k, torch_dev)
+    out = {}
+    for thr in (9, 13):
+        monkeypatch.setenv("KF_BUCKET_MIN_K", str(thr))
+        c, t = kc.count(db)
+        torch.cuda.synchronize()
+        out[thr] = (c.clone(), t.clone())
+    assert torch.equal(out[9][0], out[13][0]) and torch.equal(out[9][1], out[13][1])
