@@ -23,6 +23,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+#include <cstdio>
 #include <mutex>
 #include <vector>
 
@@ -60,6 +62,7 @@ struct BucketArgs {
     uint16_t* meta;            // gridDim.x * (nbk+1) * kRmax round bucket offsets
     uint32_t* roff;            // gridDim.x * kRmax round record offsets
     uint32_t accumulate;
+    unsigned long long* prof;   // optional (KF_BUCKET_PROFILE): per-workgroup phase cycles
 };
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
@@ -184,6 +187,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         }
 
         // ---------------------------------------------------------- phase 1
+        const uint64_t t_p1 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
         Range rg;
         uint32_t nch = 0;
         if (lo < hi) {
@@ -290,47 +294,160 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         // records and meta were stored by other waves of this workgroup: wait for
         // the stores, and read them with L1-bypassing loads below
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const uint64_t t_p2 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
         for (uint32_t i = tid; i < kRoundRecs / 2; i += kBkBlock) lds_st(L::hist + 4 * i, 0u);   // staging area
         lds_barrier();
         uint32_t* row = A.counts + (uint64_t)g * A.nbins;
         const bool split = np > 1;
         unsigned long long tsum = 0;
-        // run table of this wave: lane j <-> round wave + 16 j
+        // Run table of this wave: lane j (< nrun) <-> round wave + 16 j.  A run is
+        // the records [s, e) of one bucket in one round; it is read in 8-record
+        // (16-byte) units, and the units of all the wave's runs are laid end to end
+        // (prefix P over lanes) so every load instruction carries 64 full units
+        // whatever the run lengths.  Loads are software-pipelined one group of
+        // 4 x 64 units ahead, across bucket boundaries (the next bucket's first
+        // group is in flight during this bucket's flush).
         const uint32_t myr = (uint32_t)wave + kBkWaves * (uint32_t)lane;
         const uint32_t nrun = nround > (uint32_t)wave ? (nround - (uint32_t)wave + kBkWaves - 1) / kBkWaves : 0u;
         const uint32_t ro = myr < nround ? __builtin_nontemporal_load(roff + myr) : 0u;
-        uint32_t rs = myr < nround ? __builtin_nontemporal_load(meta + myr) : 0u;
-        for (uint32_t b = 0; b < NBK; ++b) {
-            const uint32_t re = myr < nround ? __builtin_nontemporal_load(meta + (uint64_t)(b + 1) * kRmax + myr) : 0u;
-            for (uint32_t j = 0; j < nrun; ++j) {
-                const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)rs, (int)j);
-                const uint32_t e0 = (uint32_t)__builtin_amdgcn_readlane((int)re, (int)j);
-                const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)ro, (int)j);
-                for (uint32_t q = (s0 & ~7u) + 8 * (uint32_t)lane; q < e0; q += 8 * kWave) {
-                    const v4u v = __builtin_nontemporal_load((const v4u*)(rec + base + q));
-                    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+        auto meta_at = [&](uint32_t b) -> uint32_t {
+            return myr < nround ? __builtin_nontemporal_load(meta + (uint64_t)b * kRmax + myr) : 0u;
+        };
+        struct Tbl {
+            uint32_t n, P, D, S, E;   // per lane (run)
+            uint32_t U, jc, w0;       // wave-uniform
+        };
+        auto make_tbl = [&](uint32_t rs, uint32_t re) {
+            Tbl t;
+            t.n = re > rs ? ((re + 7) >> 3) - (rs >> 3) : 0u;
+            uint32_t inc = t.n;
 #pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        const uint32_t i = q + t;
-                        if (i >= s0 && i < e0) lds_add((((d[t >> 1] >> (16 * (t & 1))) & 0xFFFFu)) << 2, 1u);
+            for (int d = 1; d < kWave; d <<= 1) {
+                const uint32_t o = __shfl_up(inc, d, kWave);
+                if (lane >= d) inc += o;
+            }
+            t.P = inc - t.n;
+            t.U = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+            t.D = ro + 8 * (rs >> 3) - 8 * t.P;   // record index of unit u = D + 8u
+            t.S = ro + rs;                        // counted records [S, E)
+            t.E = ro + re;
+            t.jc = 0;
+            t.w0 = 0;
+            return t;
+        };
+        struct Grp {
+            v4u v[4];
+            uint32_t q[4], qs[4], qe[4];
+        };
+        // next 4 windows of 64 units of table t -> loads in flight
+        auto issue = [&](Tbl& t, Grp& G) {
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                const uint32_t w0 = t.w0 + x * kWave, u = w0 + (uint32_t)lane;
+                uint32_t q = 0, qs = 0, qe = 0;
+                while (t.jc < nrun) {
+                    const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)t.P, (int)t.jc);
+                    const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)t.n, (int)t.jc);
+                    if (pj >= w0 + kWave) break;
+                    if (u >= pj && u < pj + nj) {
+                        q = (uint32_t)__builtin_amdgcn_readlane((int)t.D, (int)t.jc) + 8 * u;
+                        qs = (uint32_t)__builtin_amdgcn_readlane((int)t.S, (int)t.jc);
+                        qe = (uint32_t)__builtin_amdgcn_readlane((int)t.E, (int)t.jc);
                     }
+                    if (pj + nj > w0 + kWave) break;   // continues into the next window
+                    ++t.jc;
+                }
+                G.q[x] = q, G.qs[x] = qs, G.qe[x] = qe;
+                G.v[x] = qe > qs ? __builtin_nontemporal_load((const v4u*)(rec + q)) : v4u{0u, 0u, 0u, 0u};
+            }
+            t.w0 += 4 * kWave;
+        };
+        auto consume = [&](const Grp& G) {
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                const uint32_t d[4] = {G.v[x].x, G.v[x].y, G.v[x].z, G.v[x].w};
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const uint32_t i = G.q[x] + t;
+                    if (i >= G.qs[x] && i < G.qe[x]) lds_add(((d[t >> 1] >> (16 * (t & 1))) & 0xFFFFu) << 2, 1u);
                 }
             }
-            rs = re;
-            lds_barrier();
-            const uint32_t c1 = B.bcol[b + 1];
-            for (uint32_t col = B.bcol[b] + tid; col < c1; col += kBkBlock) {
-                const uint32_t v = lds_xchg((uint32_t)B.col_idx[col] << 2, 0u);
+        };
+        // The flush handles 4 consecutive columns per lane, lanes consecutive: one
+        // 8-byte col_idx load and one 16-byte count store per lane (coalesced
+        // rows; consecutive columns also spread the LDS reads over the banks).
+        // col_idx of up to kFG groups per lane (32768 columns: any bucket) is
+        // loaded before the barrier.
+        constexpr int kFG = 8;
+        typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+        auto flush_issue = [&](uint32_t b, v2u (&ci)[kFG]) {
+            const uint32_t c0 = B.bcol[b], c1 = B.bcol[b + 1];
+#pragma unroll
+            for (int x = 0; x < kFG; ++x) {
+                const uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + x * kBkBlock);
+                ci[x] = g4 < c1 ? *(const v2u*)(B.col_idx + g4) : v2u{0u, 0u};
+            }
+        };
+        auto flush_cols = [&](uint32_t g4, const v2u ci, uint32_t c0, uint32_t c1) {
+            if (g4 >= c1) return;
+            uint32_t v[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t col = g4 + t;
+                v[t] = (col >= c0 && col < c1) ? lds_xchg(((ci[t >> 1] >> (16 * (t & 1))) & 0xFFFFu) << 2, 0u) : 0u;
+                tsum += v[t];
+            }
+            if (!split && !B.accumulate && g4 >= c0 && g4 + 4 <= c1) {
+                *(v4u*)(row + g4) = v4u{v[0], v[1], v[2], v[3]};
+                return;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t col = g4 + t;
+                if (col < c0 || col >= c1) continue;
                 if (split) {
-                    if (v) __hip_atomic_fetch_add(row + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (v[t]) __hip_atomic_fetch_add(row + col, v[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 } else if (B.accumulate) {
-                    row[col] += v;
+                    row[col] += v[t];
                 } else {
-                    row[col] = v;
+                    row[col] = v[t];
                 }
-                tsum += v;
             }
+        };
+
+        uint32_t re_next = meta_at(1);
+        Tbl tb = make_tbl(meta_at(0), re_next);
+        re_next = NBK > 1 ? meta_at(2) : 0u;
+        Grp G0, G1;
+        issue(tb, G0);
+        uint64_t tp[4] = {0, 0, 0, 0};   // profile: records, barrier, flush, barrier
+        for (uint32_t b = 0; b < NBK; ++b) {
+            uint64_t t0 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
+            while (tb.w0 < tb.U) {          // more groups in this bucket
+                issue(tb, G1);
+                consume(G0);
+                G0 = G1;
+            }
+            consume(G0);
+            v2u ci[kFG];
+            flush_issue(b, ci);
+            if (b + 1 < NBK) {               // next bucket: table, first group in flight
+                const uint32_t rs_next = tb.E - ro;   // this bucket's run ends
+                tb = make_tbl(rs_next, re_next);
+                re_next = b + 2 < NBK ? meta_at(b + 3) : 0u;
+                issue(tb, G0);
+            }
+            if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[0] += t - t0; t0 = t; }
             lds_barrier();
+            if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[1] += t - t0; t0 = t; }
+            const uint32_t c0 = B.bcol[b], c1 = B.bcol[b + 1];
+#pragma unroll
+            for (int x = 0; x < kFG; ++x) flush_cols((c0 & ~3u) + 4 * ((uint32_t)tid + x * kBkBlock), ci[x], c0, c1);
+            for (uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + kFG * kBkBlock); g4 < c1; g4 += 4 * kBkBlock)
+                flush_cols(g4, *(const v2u*)(B.col_idx + g4), c0, c1);
+            if (B.prof) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[2] += t - t0; t0 = t; }
+            lds_barrier();
+            if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[3] += t - t0; }
         }
         tsum = wave_sum(tsum);
         unsigned long long* red = (unsigned long long*)((char*)lds + L::red);
@@ -340,6 +457,13 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             unsigned long long t = 0;
             for (int w = 0; w < kBkWaves; ++w) t += red[w];
             if (t) atomicAdd(A.totals + g, t);
+            if (B.prof) {
+                const uint64_t t_end = __builtin_amdgcn_s_memtime();
+                B.prof[8 * blockIdx.x] += t_p2 - t_p1;
+                B.prof[8 * blockIdx.x + 1] += t_end - t_p2;
+                B.prof[8 * blockIdx.x + 2] += 1;
+                for (int x = 0; x < 4; ++x) B.prof[8 * blockIdx.x + 3 + x] += tp[x];
+            }
         }
         __syncthreads();
     }
@@ -480,7 +604,15 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     B.meta = (uint16_t*)((char*)d.scratch + rec_b);
     B.roff = (uint32_t*)((char*)d.scratch + rec_b + meta_b);
     B.accumulate = (flags & KF_ACCUMULATE) ? 1u : 0u;
+    B.prof = nullptr;
     (void)nbk;
+    const char* pe = getenv("KF_BUCKET_PROFILE");   // debugging aid: synchronous, prints to stderr
+    std::vector<unsigned long long> prof_h;
+    if (pe && *pe == '1') {
+        if (hipMalloc((void**)&B.prof, (size_t)grid * 8 * 8) != hipSuccess ||
+            hipMemsetAsync(B.prof, 0, (size_t)grid * 8 * 8, s) != hipSuccess)
+            return kf_fail(KF_EHIP, "profile buffer");
+    }
     hipLaunchKernelGGL(piece_scan_kernel, dim3(1), dim3(1024), 0, s, A.goff, A.n_genomes, d.pstart);
     if (!B.accumulate)
         hipLaunchKernelGGL(zero_split_rows_kernel, dim3(1024), dim3(256), 0, s, A.goff, A.n_genomes, A.counts,
@@ -489,6 +621,20 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     if (hipLaunchKernel(fn, dim3(grid), dim3(kBkBlock), args, lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "bucket kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (hipEventRecord(d.done, s) != hipSuccess) return kf_fail(KF_EHIP, "hipEventRecord failed");
+    if (B.prof) {
+        prof_h.resize((size_t)grid * 8);
+        if (hipStreamSynchronize(s) != hipSuccess ||
+            hipMemcpy(prof_h.data(), B.prof, prof_h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+            return kf_fail(KF_EHIP, "profile readback");
+        (void)hipFree(B.prof);
+        double sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < grid; ++i)
+            for (int x = 0; x < 8; ++x) sum[x] += (double)prof_h[8 * i + x];
+        const double np = sum[2] > 0 ? sum[2] : 1;
+        fprintf(stderr, "[kf_bucket k=%d] pieces %.0f cycles/piece: phase1 %.3g phase2 %.3g "
+                "(records %.3g, barrier %.3g, flush %.3g, barrier %.3g)\n",
+                k, sum[2], sum[0] / np, sum[1] / np, sum[3] / np, sum[4] / np, sum[5] / np, sum[6] / np);
+    }
     return KF_OK;
 }
 

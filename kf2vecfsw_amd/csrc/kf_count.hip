@@ -50,14 +50,16 @@ template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 
 #endif
 // Counting modes by k:
 //   k <= 7 : one LDS histogram of all 4^k forward codes (64 KiB at k=7)
-//   k 8..9 : multi-pass LDS: the forward-code space is cut into 32768-code
+//   k = 8  : multi-pass LDS: the forward-code space is cut into 32768-code
 //            ranges (128 KiB of LDS); pass p counts codes with code >> 15 == p
-//            and its flush merges into the canonical columns (2 / 8 passes)
-//   k >= 10: global atomics at code2col[min(fwd, revcomp)]
+//            and its flush merges into the canonical columns (2 passes)
+//   k >= 9 : bucket kernels (kf_bucket.hip), see there.  The count kernels
+//            below still cover k 9..12 (multi-pass at 9, global atomics at
+//            code2col[min(fwd, revcomp)] above) for A/B runs via KF_BUCKET_MIN_K.
 constexpr int kLdsMaxK = 7;
 constexpr int kMultiMaxK = 9;
 constexpr int kMultiBits = 15;
-constexpr int kDefaultBucketMinK = 10;
+constexpr int kDefaultBucketMinK = 9;
 enum { kModeLds = 0, kModeMulti = 1, kModeGlobal = 2 };
 template <int K>
 struct ModeOf {
@@ -435,7 +437,7 @@ int block_for(int v) { return v == 0 ? Shape<0>::block : Shape<1>::block; }
 
 // KF_BUCKET_MIN_K (A-B knob, read per launch): smallest k counted by the bucket
 // kernels (kf_bucket.hip); below it k 8..9 use multi-pass LDS and k >= 10 global
-// atomics.
+// atomics.  Default 9.
 int bucket_min_k() {
     const char* e = getenv("KF_BUCKET_MIN_K");
     if (!e || !*e) return kDefaultBucketMinK;
