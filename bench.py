@@ -8,7 +8,10 @@ generated directly in HBM.  Genomes are sharded round-robin over ranks
 (rank r owns ids r, r+N, ...); no collective touches the data path.
 
 A step = one pass of the device counter over the rank's resident batch:
-zero the [genomes x 8192] count matrix + one `kf_count_batch` launch.
+zero the [genomes x 8192] count matrix + one `kf_count_batch` launch (k=7).
+The default run also times k=11 (BASELINE configs[4]) on the same batch and
+reports it under "secondary"; `roofline.traffic` is the measured HBM bytes per
+launch (rocprofv3 PMC, tools/pmc_traffic.py) when profiles/ holds it.
 `value` = all ranks' sequence characters / max-over-ranks wall time of K steps.
 `roofline.achieved` = algorithmic bytes per launch (FASTA bytes read + 4 B x
 bins written) / the count kernel's average duration,
@@ -66,6 +69,20 @@ def cpu_baseline(args, ids: list[int]) -> dict:
                       f"({el:.1f} s, oracle/kmer_oracle.c OpenMP, k={args.k})"}
 
 
+def load_traffic(k: int, workload_tag: str):
+    """Measured HBM bytes per launch (tools/pmc_traffic.py output) for this k and
+    workload, newest round under profiles/ first; None if not measured."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_k{k}.json")), reverse=True):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if t.get("k") == k and t.get("workload") == workload_tag:
+            return int(t["traffic_bytes"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,6 +95,8 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--secondary-k", type=int, default=11,
+                    help="also time this k on the same batch (BASELINE configs[4]); 0 = off; N=1 only")
     ap.add_argument("--verify", type=int, default=4, help="genomes checked bit-exactly against the oracle")
     args = ap.parse_args()
 
@@ -102,64 +121,82 @@ def main() -> None:
     g0, gs = shard_ids(n, rank, world)
     ids = C.synth_ids(n, g0, gs)
     db = C.synth_device_batch(n, args.seq_len, SEED, width=80, g0=g0, g_stride=gs, device=dev)
-    kc = C.KmerCounter(args.k, dev)
-    counts, totals = kc.alloc_out(n)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
-
     fasta_bytes = sum(C.synth_fasta_bytes(args.seq_len, 80, g) for g in ids)
-    alg_bytes = fasta_bytes + 4 * kc.nbins * n          # per launch
     bases = n * args.seq_len
+    workload_tag = f"{n} synthetic {args.seq_len / 1e6:g} Mbp genomes, 80-column FASTA"
 
-    def step(ev=None):
-        counts.zero_()
-        totals.zero_()
-        if ev is not None:
-            ev[0].record(stream)
-        kc.count(db, counts, totals, accumulate=True)
-        if ev is not None:
-            ev[1].record(stream)
+    def run(k, steps, warmup):
+        """`warmup` untimed + `steps` timed steps at k over the resident batch.
+        A step = zero the count matrix + one kf_count_batch launch.  Returns
+        (counter, counts, totals, wall s, mean kernel ms by HIP events on the
+        launch stream), both max over ranks."""
+        kc = C.KmerCounter(k, dev)
+        counts, totals = kc.alloc_out(n)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    if world > 1:
-        t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, kern_ms = float(t[0]), float(t[1])
+        # k <= 8: zero outside the events so they bracket the count kernel alone;
+        # k >= 9 (bucket kernels) write every count row, so no 4 x nbins memset
+        zero_first = k <= 8
 
-    # correctness: totals are analytic for N-free synthetic genomes; a few genomes bit-exact vs oracle
-    tot = totals.cpu().numpy()
-    ok = bool((tot == args.seq_len - args.k + 1).all())
-    if args.verify and rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import kf_oracle as O
-        cnp = C.counts_to_numpy(counts)
-        pick = np.linspace(0, n - 1, min(args.verify, n)).astype(int)
-        for i in pick:
-            c, t = O.count(O.synth_genome(ids[i], SEED + ids[i], args.seq_len, 80), args.k)
-            ok &= bool((cnp[i] == c).all()) and int(tot[i]) == t
-    if world > 1:
-        f = torch.tensor([0.0 if ok else 1.0], device=dev)
-        dist.all_reduce(f, op=dist.ReduceOp.MAX)
-        ok = float(f) == 0.0
+        def step(ev=None):
+            if zero_first:
+                counts.zero_()
+                totals.zero_()
+            if ev is not None:
+                ev[0].record(stream)
+            kc.count(db, counts, totals, accumulate=zero_first)
+            if ev is not None:
+                ev[1].record(stream)
 
-    total_bases = bases * world
-    value = total_bases / el * args.steps / 1e9
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(evs[i])
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        if world > 1:
+            t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el, kern_ms = float(t[0]), float(t[1])
+        return kc, counts, totals, el, kern_ms
+
+    def verify(k, counts, totals):
+        """totals are analytic for N-free synthetic genomes; a few genomes bit-exact vs the oracle"""
+        tot = totals.cpu().numpy()
+        ok = bool((tot == args.seq_len - k + 1).all())
+        if args.verify and rank == 0:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import kf_oracle as O
+            cnp = C.counts_to_numpy(counts)
+            pick = np.linspace(0, n - 1, min(args.verify, n)).astype(int)
+            for i in pick:
+                c, t = O.count(O.synth_genome(ids[i], SEED + ids[i], args.seq_len, 80), k)
+                ok &= bool((cnp[i] == c).all()) and int(tot[i]) == t
+        if world > 1:
+            f = torch.tensor([0.0 if ok else 1.0], device=dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            ok = float(f) == 0.0
+        return ok
+
+    kc, counts, totals, el, kern_ms = run(args.k, args.steps, args.warmup)
+    alg_bytes = fasta_bytes + 4 * kc.nbins * n          # per launch (SURVEY 8(d))
+    ok = verify(args.k, counts, totals)
     grid, block, lds = kc.launch_info()
+    del counts, totals
+
+    value = bases * world / el * args.steps / 1e9
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(args.k, workload_tag)
     out = {
         "metric": "Gbases/s k-mer→.kf build at k=7; achieved HBM GB/s vs gfx950 peak",
         "value": round(value, 3),
@@ -179,10 +216,29 @@ def main() -> None:
                    "global_batch": n * world, "parallelism": f"round-robin genome shards x{world}, no collective",
                    "kernel_grid": [grid, block], "lds_bytes": lds},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": None,
+                     "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": int(alg_bytes)},
         "parity": "ok" if ok else "MISMATCH",
     }
+    if args.secondary_k and world == 1 and args.secondary_k != args.k:
+        k2 = args.secondary_k
+        kc2, c2, t2, el2, km2 = run(k2, max(3, args.steps // 4), 1)
+        ok2 = verify(k2, c2, t2)
+        ok &= ok2
+        alg2 = fasta_bytes + 4 * kc2.nbins * n
+        tr2, src2 = load_traffic(k2, workload_tag)
+        out["secondary"] = {
+            "config": f"1xMI355X, k={k2} (BASELINE configs[4]), same batch",
+            "value": round(bases / el2 * max(3, args.steps // 4) / 1e9, 3), "unit": "Gbases/s",
+            "ms_per_step": round(el2 / max(3, args.steps // 4) * 1e3, 4),
+            "roofline": {"bound": "hbm", "achieved": round(alg2 / (km2 * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBPS,
+                         "unit": "GB/s", "frac": round(alg2 / (km2 * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+                         "traffic": tr2, "traffic_source": src2, "kernel_ms": round(km2, 4),
+                         "alg_bytes_per_launch": int(alg2)},
+            "parity": "ok" if ok2 else "MISMATCH"}
+        out["parity"] = "ok" if ok else "MISMATCH"
+        del c2, t2
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, ids)
     if rank == 0:

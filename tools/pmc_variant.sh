@@ -2,7 +2,7 @@
 # PMC passes on tools/ab_bench.py for one KF_COUNT_VARIANT (VARIANT env), counters from GROUPS_LIST.
 set -u
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$REPO/gpurun_out/pmcv${VARIANT}
+OUT=$REPO/gpurun_out/${PMC_TAG:-pmcv$VARIANT}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 i=0
