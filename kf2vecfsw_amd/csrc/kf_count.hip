@@ -25,6 +25,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <cstdio>
+
 #include "kf_front.h"
 #include "kf_internal.h"
 
@@ -183,8 +185,14 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
                                                   uint32_t* __restrict__ hist, uint32_t pass) {
     if (lo >= hi) return 0;
     uint32_t* gcounts = GLOBAL ? A.counts + (uint64_t)g * A.nbins : nullptr;
+    const uint64_t t_begin = A.prof ? __builtin_amdgcn_s_memtime() : 0;
     Range rg;
     rg.begin<K>(A, glo, ghi, lo, hi, lane);
+    uint64_t t_loop = 0;
+    if (A.prof) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        t_loop = __builtin_amdgcn_s_memtime();
+    }
     uint32_t carry = rg.carry;
     uint32_t rel = 0;
     const ChunkMask m = rg.mask();
@@ -223,6 +231,16 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
     if (rem > 0) count(b0);
     if (rem > 1) count(b1);
     if (rem > 2) count(b2);
+    if (A.prof && lane == 0) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const uint64_t t_end = __builtin_amdgcn_s_memtime();
+        const int w = (int)(threadIdx.x >> 6);
+        atomicAdd(A.prof + 0, (unsigned long long)(t_loop - t_begin));
+        atomicAdd(A.prof + 1, (unsigned long long)(t_end - t_loop));
+        atomicAdd(A.prof + 2, 1ull);
+        atomicAdd(A.prof + 8 + w, (unsigned long long)(t_end - t_loop));
+        atomicAdd(A.prof + 24 + w, (unsigned long long)nch);
+    }
     return lane_total;
 }
 
@@ -284,7 +302,9 @@ __global__ void __launch_bounds__(Shape<V>::block)
         for (uint32_t pass = 0; pass < (uint32_t)ModeOf<K>::passes; ++pass) {
             const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl>(A, g, glo, ghi, lo_c, hi_c, lane, hist, pass);
             if (Shape<V>::abl) asm volatile("" ::"v"((uint32_t)lt));   // keep ablated work alive
+            const uint64_t t_f0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             __syncthreads();
+            const uint64_t t_f1 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             // canonical bin = forward count of the k-mer + forward count of its
             // revcomp; coalesced u32 atomics in column order
             for (uint32_t col = tid; col < A.nbins; col += kBlock) {
@@ -314,7 +334,15 @@ __global__ void __launch_bounds__(Shape<V>::block)
                     s += v;
                 }
             }
+            const uint64_t t_f2 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             __syncthreads();
+            if (A.prof && tid == 0) {
+                const uint64_t t_f3 = __builtin_amdgcn_s_memtime();
+                atomicAdd(A.prof + 3, (unsigned long long)(t_f1 - t_f0));
+                atomicAdd(A.prof + 4, 1ull);
+                atomicAdd(A.prof + 5, (unsigned long long)(t_f2 - t_f1));
+                atomicAdd(A.prof + 6, (unsigned long long)(t_f3 - t_f2));
+            }
         }
         s = wave_sum(s);
         if (lane == 0) red[wave] = s;
@@ -531,6 +559,12 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.totals = (unsigned long long*)d_totals;
     A.nbins = (uint32_t)nb;
     A.n_genomes = n_genomes;
+    A.prof = nullptr;
+    const char* pe = getenv("KF_COUNT_PROFILE");   // debugging aid: synchronous, prints to stderr
+    if (pe && *pe == '1' && !bucket) {
+        if (hipMalloc((void**)&A.prof, 40 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 40 * 8, s) != hipSuccess)
+            return kf_fail(KF_EHIP, "profile buffer");
+    }
     if (bucket) return bucket_launch(A, k, flags, s);
     int grid = 0, block = 0, lds = 0, variant = 0;
     int rc = launch_info(k, &grid, &block, &lds, &variant);
@@ -538,6 +572,20 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     void* args[] = {&A};
     if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (A.prof) {
+        unsigned long long h[40];
+        if (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(h, A.prof, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
+            return kf_fail(KF_EHIP, "profile readback");
+        (void)hipFree(A.prof);
+        const double nf = h[4] ? (double)h[4] : 1.0, nr = h[2] ? (double)h[2] : 1.0;
+        fprintf(stderr, "[count_kernel k=%d] wave ranges %llu: setup %.3g cyc/range, loop %.3g cyc/range; "
+                "flushes %llu (wave 0): barrier-in %.3g, flush %.3g, barrier-out %.3g cyc\n", k, h[2],
+                (double)h[0] / nr, (double)h[1] / nr, h[4], (double)h[3] / nf, (double)h[5] / nf, (double)h[6] / nf);
+        for (int w = 0; w < 16; ++w)
+            if (h[24 + w])
+                fprintf(stderr, "  wave %2d: %.0f cyc/chunk over %llu chunks\n", w, (double)h[8 + w] / h[24 + w],
+                        h[24 + w]);
+    }
     return KF_OK;
 }
 

@@ -22,6 +22,7 @@ struct CountArgs {
     unsigned long long* totals;
     uint32_t nbins;
     int32_t n_genomes;
+    unsigned long long* prof;      // optional cycle counters (KF_COUNT_PROFILE=1), else null
 };
 
 // ---------------------------------------------------------------- tails
