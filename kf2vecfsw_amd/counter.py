@@ -124,9 +124,10 @@ def pack_genomes(blobs: Sequence[bytes | np.ndarray], names: Sequence[str] | Non
 
 
 def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: int = N.KF_FMT_AUTO,
-               pin: bool = True, threads: int = 8) -> HostBatch:
+               pin: bool = True, threads: int = 8, pool=None) -> HostBatch:
     """Read files straight into one (pinned) buffer and index their records; files
-    are read and indexed by a thread pool (readinto and the ctypes call release the GIL)."""
+    are read and indexed by a thread pool (readinto and the ctypes call release the
+    GIL): `pool` if given (shared across batches), else one of `threads` workers."""
     from concurrent.futures import ThreadPoolExecutor
     sizes = [os.path.getsize(p) for p in paths]
     off = _layout(sizes)
@@ -146,7 +147,9 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
         d[lo + sz: int(off[i + 1])] = 10
         return index_records(d[lo: lo + sz], fmt, lo)[0]
 
-    if threads > 1 and len(paths) > 1:
+    if pool is not None:
+        excl = list(pool.map(one, range(len(paths))))
+    elif threads > 1 and len(paths) > 1:
         with ThreadPoolExecutor(max_workers=min(threads, len(paths))) as ex:
             excl = list(ex.map(one, range(len(paths))))
     else:

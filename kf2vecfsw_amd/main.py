@@ -62,6 +62,15 @@ def format_kf(name: str, counts: np.ndarray, pseudocount: bool = False, raw_cnt:
     return buf.raw[: w.value]
 
 
+def _pipeline_budget(paths: list[str], batch_gb) -> int:
+    """Bytes per batch: -batch_gb if given, else about a quarter of the input
+    (so reading, copying, counting and writing overlap) within [32 MiB, 4 GiB]."""
+    if batch_gb:
+        return int(float(batch_gb) * (1 << 30))
+    total = sum(os.path.getsize(p) for p in paths)
+    return int(min(max(total // 4, 32 << 20), 4 << 30))
+
+
 def _batches(paths: list[str], budget: int) -> list[list[int]]:
     out, cur, size = [], [], 0
     for i, p in enumerate(paths):
@@ -94,43 +103,66 @@ def get_frequencies(args) -> None:
             args.k, supported_k.start, supported_k.stop - 1))
 
     import torch
-    from .counter import KmerCounter, counts_to_numpy, pack_files, to_device
+    from .counter import KmerCounter, pack_files, to_device
 
     device = torch.device(getattr(args, "device", None) or "cuda")
     counter = KmerCounter(args.k, device)
-    budget = int(float(getattr(args, "batch_gb", 4.0) or 4.0) * (1 << 30))
     paths = [os.path.join(args.input_dir, f) for f in files_names]
+    batches = _batches(paths, _pipeline_budget(paths, getattr(args, "batch_gb", None)))
     # the reference processes files in order and later ones overwrite earlier
     # ones with the same sample name: keep the last occurrence only
     last = {s: i for i, s in enumerate(samples_names)}
-    batches = _batches(paths, budget)
     threads = max(1, int(args.p))
+    from collections import deque
     from concurrent.futures import ThreadPoolExecutor
 
-    def pack(idx):
-        return pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], threads=threads)
+    files_pool = ThreadPoolExecutor(max_workers=threads)
 
-    # pipeline: the next batch is read + indexed while this one is counted and written
-    prefetch = ThreadPoolExecutor(max_workers=1)
-    fut = prefetch.submit(pack, batches[0]) if batches else None
+    def pack(idx):
+        return pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool)
+
+    # Three-stage pipeline over batches:
+    #   readers (2)   : read + record-index batches i+1, i+2 into pinned memory
+    #                   (one shared pool of -p file workers keeps all cores busy)
+    #   this thread   : H2D + count + D2H of batch i on a side stream (async)
+    #   writer thread : wait for batch i's copy-back, format + write its .kf files
+    # The prints stay in the reference's per-file order (main.py:332-341).
+    stream = torch.cuda.Stream(device)
+    reader = ThreadPoolExecutor(max_workers=2)
+    writer = ThreadPoolExecutor(max_workers=1)
+    reads = deque(reader.submit(pack, batches[i]) for i in range(min(2, len(batches))))
+    writes = []
+
+    def write(ev, host, hb, names):
+        ev.synchronize()
+        c = host.numpy().view(np.uint32)
+        write_kf_files(args.output_dir, names, c, args.pseudocount, args.raw_cnt, args.p)
+        del hb   # pinned input stays alive until the copies that read it are done
+
     for bi, idx in enumerate(batches):
-        hb = fut.result()
-        if bi + 1 < len(batches):
-            fut = prefetch.submit(pack, batches[bi + 1])
-        db = to_device(hb, device)
-        counts, _ = counter.count(db)
-        c = counts_to_numpy(counts)
-        keep = []
-        for j, i in enumerate(idx):
+        hb = reads.popleft().result()
+        if bi + 2 < len(batches):
+            reads.append(reader.submit(pack, batches[bi + 2]))
+        with torch.cuda.stream(stream):
+            db = to_device(hb, device)
+            counts, _ = counter.count(db, stream=stream.cuda_stream)
+            keep = [j for j, i in enumerate(idx) if last[samples_names[i]] == i]
+            rows = counts if len(keep) == len(idx) else counts[torch.tensor(keep, device=device)]
+            host = torch.empty(rows.shape, dtype=rows.dtype, pin_memory=True)
+            host.copy_(rows, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        for i in idx:
             if args.pseudocount:                       # main.py:332-333
                 print(">>> Adding pseudocounts. Sample: {}".format(files_names[i]))
             if not args.raw_cnt:                       # main.py:340-341
                 print(">>> Normalizing. Sample: {}".format(files_names[i]))
-            if last[samples_names[i]] == i:
-                keep.append(j)
-        write_kf_files(args.output_dir, [samples_names[idx[j]] for j in keep], c[keep],
-                       args.pseudocount, args.raw_cnt, args.p)
-    prefetch.shutdown()
+        writes.append(writer.submit(write, ev, host, hb, [samples_names[idx[j]] for j in keep]))
+    for w in writes:
+        w.result()
+    reader.shutdown()
+    writer.shutdown()
+    files_pool.shutdown()
 
     print("\n==> Done processing {}".format(args.input_dir))
 
@@ -315,7 +347,8 @@ def build_parser() -> argparse.ArgumentParser:
     pf.add_argument("-pseudocount", action="store_true",
                     help="Computes k-mer counts with 0.5 pseudocount added to each frequency value")
     pf.add_argument("-raw_cnt", action="store_true", help="Computes raw k-mer counts without normalization")
-    pf.add_argument("-batch_gb", type=float, default=4.0, help="Input bytes per device batch (GiB). Default: 4")
+    pf.add_argument("-batch_gb", type=float, default=None,
+                    help="Input bytes per device batch (GiB). Default: about 1/4 of the input, 32 MiB..4 GiB")
     pf.add_argument("-device", default=None, help="torch device (default: cuda)")
     pf.set_defaults(func=get_frequencies)
 

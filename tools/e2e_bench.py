@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default="/tmp/kf_e2e")
     ap.add_argument("--k", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     import torch
     import kf_oracle as O
@@ -75,9 +76,14 @@ def main():
 
     cli = ["get_frequencies", "-input_dir", inp, "-output_dir", out, "-k", str(args.k), "-p", str(args.threads)]
     M.main(cli)                       # warm: runtime init, kernel load, page cache
-    t0 = time.perf_counter()
-    M.main(cli)
-    cli_s = time.perf_counter() - t0
+    # A/B in one process: the pipelined default (auto batch size) vs one batch
+    walls = {"pipelined": [], "one_batch": []}
+    for _ in range(args.reps):
+        for tag, extra in (("pipelined", []), ("one_batch", ["-batch_gb", "64"])):
+            t0 = time.perf_counter()
+            M.main(cli + extra)
+            walls[tag].append(time.perf_counter() - t0)
+    cli_s = min(walls["pipelined"])
 
     # phase breakdown on the same files
     dev = torch.device("cuda:0")
@@ -101,6 +107,7 @@ def main():
     res = {"config": f"1xMI355X, k={args.k}, {args.genomes} bacterial-like .fna (~5 Mbp, 1-80 contigs)",
            "bytes": int(sum(sizes)), "seq_chars": int(bases), "gen_s": round(gen_s, 2),
            "cli_wall_s": round(cli_s, 4), "cli_Gbases_s": round(bases / cli_s / 1e9, 3),
+           "cli_wall_s_all": {k: [round(x, 4) for x in v] for k, v in walls.items()},
            "phases_s": {k: round(v, 5) for k, v in ph.items()},
            "kernel_Gbases_s": round(bases / ph["kernel"] / 1e9, 1),
            "h2d_GBps": round(sum(sizes) / ph["h2d"] / 1e9, 1),
