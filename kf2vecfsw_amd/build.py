@@ -30,7 +30,7 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, ablation: bool = False, out: str | None = None) -> str:
-    """ablation=True adds profiling-only kernel variants (KF_COUNT_VARIANT 2, 3)."""
+    """ablation=True adds profiling-only kernel variants (KF_COUNT_VARIANT 3, 4)."""
     out = out or OUT
     if not force and not ablation and out == OUT and not _stale():
         return OUT

@@ -36,19 +36,21 @@ namespace kf {
 // waves of a workgroup, so a bigger workgroup raises occupancy at equal LDS.
 //   variant 0: 512 threads (8 waves), 2 workgroups/CU at k=7
 //   variant 1: 1024 threads (16 waves), 8 waves/SIMD register budget
+//   variant 2: as 1 with a 6-deep chunk prefetch ring (5 chunks in flight)
 #ifdef KF_ABLATION
-constexpr int kNumVariants = 4;
+constexpr int kNumVariants = 5;
 #else
-constexpr int kNumVariants = 2;
+constexpr int kNumVariants = 3;
 #endif
 constexpr int kDefaultVariant = 1;
 template <int V> struct Shape;
-template <> struct Shape<0> { static constexpr int block = 512, wpe = 0, abl = 0; };
-template <> struct Shape<1> { static constexpr int block = 1024, wpe = 8, abl = 0; };
+template <> struct Shape<0> { static constexpr int block = 512, wpe = 0, abl = 0, ring = 4; };
+template <> struct Shape<1> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 4; };
+template <> struct Shape<2> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 6; };
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
-template <> struct Shape<2> { static constexpr int block = 1024, wpe = 8, abl = 1; };   // no LDS adds
-template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 3; };   // stream bytes only
+template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 1, ring = 4; };   // no LDS adds
+template <> struct Shape<4> { static constexpr int block = 1024, wpe = 8, abl = 3, ring = 4; };   // stream only
 #endif
 // Counting modes by k:
 //   k <= 7 : one LDS histogram of all 4^k forward codes (64 KiB at k=7)
@@ -80,37 +82,36 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
                                                 uint32_t& lane_total, uint32_t pass) {
     constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
     constexpr int W2 = 2 * K;
-    uint32_t C, V, EN, ne, own;
-    front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
-
     if constexpr (ModeOf<K>::mode == kModeLds && !MASKED && ABL == 0) {
-        // Fast case (uniform, the common one): in every lane the block holds
-        // 15 or 16 entries (at most one newline), all valid, and the last k-1
-        // entries of lane L-1 (lane 0: the carry) are valid.  Then windows
+        // Fast case (uniform, the common one): every lane's 16 bytes are bases
+        // except at most one newline, and the carry is complete.  Then every
+        // lane's 15-16 entries are valid, so is lane L-1's tail, windows
         // 0..ne-1 are valid and the context is just lane L-1's raw codes: no
-        // tails, no run mask, no inc extraction.  Test: V (zero above ne-1)
-        // must be 0x7FFF with ne == 15 or 0xFFFF with ne == 16, i.e.
-        // V ^ (ne == 16 ? 0x8000 : 0) == 0x7FFF.
-        constexpr uint32_t KM = (1u << (K - 1)) - 1u;
-        constexpr uint32_t FM = (KM << 16) | 0xFFFFu, FT = (KM << 16) | 0x7FFFu;
-        const uint32_t pC = wave_shr1(t_codes(carry), C);
-        const uint32_t pV = wave_shr1(t_n(carry) >= (uint32_t)(K - 1) ? KM : 0u, V);
-        const bool lane_ok = ((((pV << 16) | V) ^ ((ne << 11) & 0x8000u)) & FM) == FT;
-        if (__builtin_amdgcn_ballot_w64(!lane_ok) == 0) {
+        // validity masks, no tails, no run mask, no inc extraction.
+        uint32_t Cf, NNL, bad;
+        classify16_fast(d, Cf, NNL, bad);
+        const uint32_t nef = (uint32_t)__builtin_popcount(NNL);
+        const bool self_ok = bad == 0 && nef >= 15u;
+        if (t_n(carry) >= (uint32_t)(K - 1) && __builtin_amdgcn_ballot_w64(!self_ok) == 0) {
+            // drop the newline entry (none: r = 16, identity)
+            const uint32_t r = (uint32_t)__builtin_ctz((NNL ^ 0xFFFFu) | 0x10000u);
+            const uint32_t lo1 = (1u << r) - 1u, lo2 = lo1 | (lo1 << r);
+            const uint32_t C = bfi(lo2, Cf, Cf >> 2);
+            const uint32_t pC = wave_shr1(t_codes(carry), C);
             // X = (pC:C) << 2 over ne entries of C; ne in {15, 16} and C is zero
             // above entry ne-1, so the high word is pC << (2ne+2 mod 32) | C >> 30.
             // Byte address of window r = bits [2r, 2r+2K+2) of X, masked: 8
             // views at bit offsets 0,2,..,14 serve r = 0..7 from their low 16
             // bits and r = 8..15 from their high 16 bits (a word select).
             constexpr uint32_t M4 = ((1u << W2) - 1u) << 2;
-            const uint32_t xlo = C << 2, xhi = (pC << ((2u * ne + 2u) & 31u)) | (C >> 30);
+            const uint32_t xlo = C << 2, xhi = (pC << ((2u * nef + 2u) & 31u)) | (C >> 30);
             uint32_t xv[8];
 #pragma unroll
             for (int o = 0; o < 8; ++o) xv[o] = o ? __builtin_amdgcn_alignbit(xhi, xlo, 2 * o) : xlo;
-            auto addr = [&](int r) -> uint32_t { return (r < 8 ? xv[r] : (xv[r - 8] >> 16)) & M4; };
-            const uint32_t inc15 = V >> 15;   // == (ne == 16)
+            auto addr = [&](int w) -> uint32_t { return (w < 8 ? xv[w] : (xv[w - 8] >> 16)) & M4; };
+            const uint32_t inc15 = nef >> 4;   // window 15 exists iff no newline
 #pragma unroll
-            for (int r = 0; r < 15; ++r) lds_add(addr(r), 1u);
+            for (int w = 0; w < 15; ++w) lds_add(addr(w), 1u);
             lds_add(addr(15), inc15);
             lane_total += 15u + inc15;
             // lane 63's block is all valid bases: its tail is complete
@@ -118,6 +119,8 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
             return tail_pack(c63 & TM, 31u, 31u);
         }
     }
+    uint32_t C, V, EN, ne, own;
+    front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
     const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
     const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
     const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
@@ -179,7 +182,7 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
 }
 
 // Process the wave range [lo, hi) of genome [glo, ghi).
-template <int K, bool GLOBAL, int ABL>
+template <int K, bool GLOBAL, int ABL, int RING>
 __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                   uint64_t lo, uint64_t hi, int lane,
                                                   uint32_t* __restrict__ hist, uint32_t pass) {
@@ -197,40 +200,37 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
     uint32_t rel = 0;
     const ChunkMask m = rg.mask();
     uint32_t lane_total = 0;
-    // 4-deep ring, 3 chunks in flight while one is counted; a buffer is refilled
-    // only after it has been consumed, so no register rotation waits on a load
-    uint4 b0 = rg.load(A.bytes, 0, lane);
-    uint4 b1 = rg.load(A.bytes, kChunk, lane);
-    uint4 b2 = rg.load(A.bytes, 2 * kChunk, lane);
-    uint4 b3 = rg.load(A.bytes, 3 * kChunk, lane);
-    auto count = [&](const uint4 buf) {
+    // RING-deep register ring, RING-1 chunks in flight while one is counted; a
+    // buffer is refilled only after it has been consumed, so no register
+    // rotation waits on a load
+    uint4 buf[RING];
+#pragma unroll
+    for (int j = 0; j < RING; ++j) buf[j] = rg.load(A.bytes, j * kChunk, lane);
+    auto count = [&](const uint4 bf) {
         const uint64_t cc = rg.c0 + rel;
         const bool msk = rg.masked(A, rel);
         if (ABL == 3) {          // profiling only: stream the bytes, no counting
-            lane_total += buf.x ^ buf.y ^ buf.z ^ buf.w;
+            lane_total += bf.x ^ bf.y ^ bf.z ^ bf.w;
         } else if (msk)
-            carry = count_chunk<K, true, GLOBAL, ABL>(buf, A, cc, lane, m, rg.iv, carry, hist, gcounts, lane_total, pass);
+            carry = count_chunk<K, true, GLOBAL, ABL>(bf, A, cc, lane, m, rg.iv, carry, hist, gcounts, lane_total, pass);
         else
-            carry = count_chunk<K, false, GLOBAL, ABL>(buf, A, cc, lane, m, rg.iv, carry, hist, gcounts, lane_total, pass);
+            carry = count_chunk<K, false, GLOBAL, ABL>(bf, A, cc, lane, m, rg.iv, carry, hist, gcounts, lane_total, pass);
         rel += kChunk;
     };
-    // steady state: groups of 4 chunks with no exit in between (keeps the
+    // steady state: groups of RING chunks with no exit in between (keeps the
     // compiler's vmcnt bookkeeping exact: wait for the oldest load only)
     const uint32_t nch = rg.nch;
-    for (uint32_t i = 0; i + 4 <= nch; i += 4) {
-        count(b0);
-        b0 = rg.load(A.bytes, rel + 3 * kChunk, lane);
-        count(b1);
-        b1 = rg.load(A.bytes, rel + 3 * kChunk, lane);
-        count(b2);
-        b2 = rg.load(A.bytes, rel + 3 * kChunk, lane);
-        count(b3);
-        b3 = rg.load(A.bytes, rel + 3 * kChunk, lane);
+    for (uint32_t i = 0; i + RING <= nch; i += RING) {
+#pragma unroll
+        for (int j = 0; j < RING; ++j) {
+            count(buf[j]);
+            buf[j] = rg.load(A.bytes, rel + (RING - 1) * kChunk, lane);
+        }
     }
-    const uint32_t rem = nch & 3;
-    if (rem > 0) count(b0);
-    if (rem > 1) count(b1);
-    if (rem > 2) count(b2);
+    const uint32_t rem = nch % RING;
+#pragma unroll
+    for (int j = 0; j < RING - 1; ++j)
+        if (rem > (uint32_t)j) count(buf[j]);
     if (A.prof && lane == 0) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         const uint64_t t_end = __builtin_amdgcn_s_memtime();
@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
         // wave w owns [split(w), split(w+1)): 16-byte aligned, monotone, covering [plo, phi)
         const uint64_t lo_c = split_at(plo, phi, wave, kWaves), hi_c = split_at(plo, phi, wave + 1, kWaves);
         if (GLOBAL) {
-            const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
+            const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl, Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
             const unsigned long long s = wave_sum(lt);
             if (lane == 0 && s) atomicAdd(A.totals + g, s);
             continue;
@@ -300,7 +300,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
         unsigned long long s = 0;
         uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
         for (uint32_t pass = 0; pass < (uint32_t)ModeOf<K>::passes; ++pass) {
-            const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl>(A, g, glo, ghi, lo_c, hi_c, lane, hist, pass);
+            const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl, Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane, hist, pass);
             if (Shape<V>::abl) asm volatile("" ::"v"((uint32_t)lt));   // keep ablated work alive
             const uint64_t t_f0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             __syncthreads();
@@ -456,12 +456,13 @@ void* count_kernel_v(int k) {
 
 void* count_kernel_for(int k, int v) {
 #ifdef KF_ABLATION
-    if (v == 2) return count_kernel_v<2>(k);
     if (v == 3) return count_kernel_v<3>(k);
+    if (v == 4) return count_kernel_v<4>(k);
 #endif
+    if (v == 2) return count_kernel_v<2>(k);
     return v == 0 ? count_kernel_v<0>(k) : count_kernel_v<1>(k);
 }
-int block_for(int v) { return v == 0 ? Shape<0>::block : Shape<1>::block; }
+int block_for(int v) { return v == 0 ? Shape<0>::block : Shape<1>::block; }   // all others 1024
 
 // KF_BUCKET_MIN_K (A-B knob, read per launch): smallest k counted by the bucket
 // kernels (kf_bucket.hip); below it k 8..9 use multi-pass LDS and k >= 10 global

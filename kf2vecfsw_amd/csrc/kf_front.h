@@ -86,6 +86,33 @@ __device__ __forceinline__ void classify16(const uint4 d, uint32_t& C, uint32_t&
     NNL = (pair(nf[0], nf[1]) << 8) | pair(nf[2], nf[3]);   // not-newline mask
 }
 
+// Fast-path flavour of classify16: codes C, not-newline mask NNL, and `bad`,
+// non-zero iff some byte is neither a base nor a newline (OR of vf & nf).
+__device__ __forceinline__ void classify16_fast(const uint4 d, uint32_t& C, uint32_t& NNL, uint32_t& bad) {
+    const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+    uint32_t pc[4], nf[4];
+    bad = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = w[q];
+        const uint32_t cb = (x >> 1) & 0x03030303u;
+        const uint32_t ex = __builtin_amdgcn_perm(0u, 0x4B584F4Du, cb);
+        const uint32_t y = (x ^ ex) & 0xDFDFDFDFu;
+        const uint32_t vf = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, y);
+        nf[q] = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, x ^ 0x06060606u);
+        bad |= vf & nf[q];
+        pc[q] = __builtin_amdgcn_udot4(cb, 0x01041040u, 0u, false);
+    }
+    const uint32_t c01 = __builtin_amdgcn_perm(pc[0], pc[1], 0x0C0C0400u);
+    const uint32_t c23 = __builtin_amdgcn_perm(pc[2], pc[3], 0x0C0C0400u);
+    C = (c01 << 16) | c23;
+    auto pair = [](const uint32_t a, const uint32_t b) -> uint32_t {
+        return (uint32_t)__builtin_amdgcn_sdot4((int)a, (int)0xF0E0C080u,
+                                               __builtin_amdgcn_sdot4((int)b, (int)0xFFFEFCF8u, 0, false), false);
+    };
+    NNL = (pair(nf[0], nf[1]) << 8) | pair(nf[2], nf[3]);
+}
+
 // Remove newline entries (compaction).  C: 2-bit entries, V/EN: 1-bit masks,
 // entry r at bits [2r, 2r+2) / bit r.  The lowest newline is removed branch-free
 // (r = 16 sentinel when there is none: every mask becomes the identity); any
