@@ -30,11 +30,21 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, ablation: bool = False, out: str | None = None) -> str:
-    """ablation=True adds profiling-only kernel variants (KF_COUNT_VARIANT 3, 4)."""
+    """ablation=True adds profiling-only kernel variants (KF_COUNT_VARIANT 3, 4).
+    Serialised by a file lock: every rank of a multi-process run may call it."""
+    import fcntl
     out = out or OUT
     if not force and not ablation and out == OUT and not _stale():
         return OUT
     os.makedirs(BUILD, exist_ok=True)
+    with open(os.path.join(BUILD, ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and not ablation and out == OUT and not _stale():   # another rank built it
+            return OUT
+        return _build_locked(verbose, ablation, out)
+
+
+def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
     objs = []
     for s in SOURCES_HIP:
         o = os.path.join(BUILD, s + ".o")
