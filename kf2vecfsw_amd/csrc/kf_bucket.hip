@@ -166,15 +166,8 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
 
     for (uint32_t p = blockIdx.x; p < npiece; p += gridDim.x) {
         // genome of piece p: last g with pstart[g] <= p
-        int32_t g;
-        {
-            int32_t a = 0, e = A.n_genomes - 1;
-            while (a < e) {
-                const int32_t mid = (a + e + 1) >> 1;
-                if (B.pstart[mid] <= p) a = mid; else e = mid - 1;
-            }
-            g = a;
-        }
+        const int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, p, lane,
+                                                    [&](uint64_t i) { return (uint64_t)B.pstart[i]; }) - 1;
         const uint32_t np = B.pstart[g + 1] - B.pstart[g], pi = p - B.pstart[g];
         const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
         const uint64_t plo = split_at(glo, ghi, pi, np), phi = split_at(glo, ghi, pi + 1, np);
@@ -191,16 +184,17 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         Range rg;
         uint32_t nch = 0;
         if (lo < hi) {
-            rg.begin<K>(A, glo, ghi, lo, hi, lane);
+            rg.init(glo, ghi, lo, hi);
             nch = rg.nch;
         }
-        uint32_t carry = lo < hi ? rg.carry : 0u;
-        uint32_t off = 0;   // records written so far (multiple of 8)
-        uint32_t rel = 0;
-        uint4 buf[4];
+        uint4 buf[4];   // the first chunks go out before the warm-up's dependent loads
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             buf[j] = (uint32_t)j < nch ? rg.load(A.bytes, j * kChunk, lane) : make_uint4(0u, 0u, 0u, 0u);
+        if (lo < hi) rg.warm<K>(A, lane);
+        uint32_t carry = lo < hi ? rg.carry : 0u;
+        uint32_t off = 0;   // records written so far (multiple of 8)
+        uint32_t rel = 0;
         auto round = [&](uint32_t r, uint4& bf) {
             uint32_t s[16], rk[16];
             const bool have = r < nch;

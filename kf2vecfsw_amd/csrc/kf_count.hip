@@ -190,7 +190,14 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
     uint32_t* gcounts = GLOBAL ? A.counts + (uint64_t)g * A.nbins : nullptr;
     const uint64_t t_begin = A.prof ? __builtin_amdgcn_s_memtime() : 0;
     Range rg;
-    rg.begin<K>(A, glo, ghi, lo, hi, lane);
+    rg.init(glo, ghi, lo, hi);
+    // RING-deep register ring, RING-1 chunks in flight while one is counted; a
+    // buffer is refilled only after it has been consumed, so no register
+    // rotation waits on a load.  The first loads go out before the warm-up.
+    uint4 buf[RING];
+#pragma unroll
+    for (int j = 0; j < RING; ++j) buf[j] = rg.load(A.bytes, j * kChunk, lane);
+    rg.warm<K>(A, lane);
     uint64_t t_loop = 0;
     if (A.prof) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -200,12 +207,6 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
     uint32_t rel = 0;
     const ChunkMask m = rg.mask();
     uint32_t lane_total = 0;
-    // RING-deep register ring, RING-1 chunks in flight while one is counted; a
-    // buffer is refilled only after it has been consumed, so no register
-    // rotation waits on a load
-    uint4 buf[RING];
-#pragma unroll
-    for (int j = 0; j < RING; ++j) buf[j] = rg.load(A.bytes, j * kChunk, lane);
     auto count = [&](const uint4 bf) {
         const uint64_t cc = rg.c0 + rel;
         const bool msk = rg.masked(A, rel);
@@ -275,15 +276,8 @@ __global__ void __launch_bounds__(Shape<V>::block)
                                           : base + ((total / G * (b + 1) + (total % G) * (b + 1) / G) & ~(uint64_t)15);
     if (span_lo >= span_hi) return;
     // first genome whose end is beyond span_lo
-    int32_t g;
-    {
-        int32_t a = 0, e = A.n_genomes;
-        while (a < e) {
-            const int32_t mid = (a + e) >> 1;
-            if (A.goff[mid + 1] <= span_lo) a = mid + 1; else e = mid;
-        }
-        g = a;
-    }
+    int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, span_lo, lane,
+                                          [&](uint64_t i) { return A.goff[i + 1]; });
     for (; g < A.n_genomes; ++g) {
         const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
         if (glo >= span_hi) break;

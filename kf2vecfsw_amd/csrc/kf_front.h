@@ -265,6 +265,25 @@ __device__ __forceinline__ void front_end(const uint4 d, const CountArgs& A, uin
     if (OWN) own = own_tail<K>(C, V, ne);
 }
 
+// Index of the first element of a non-decreasing sequence key(0..n) with
+// key(i) > x (n if none), by a 64-way wave-parallel search: one load latency per
+// 64x narrowing instead of one per halving (log64 n vs log2 n dependent loads).
+// Wave-uniform arguments; every lane must be active.
+template <class KeyF>
+__device__ __forceinline__ uint64_t wave_upper_bound(uint64_t n, uint64_t x, int lane, KeyF key) {
+    uint64_t a = 0, b = n;   // the answer lies in [a, b]
+    while (b - a > (uint64_t)kWave) {
+        const uint64_t step = (b - a + kWave - 1) / kWave;
+        const uint64_t i = a + step * (uint64_t)lane;
+        const uint32_t cnt = (uint32_t)__builtin_popcountll(__ballot(i < b && key(i) <= x));
+        const uint64_t na = cnt ? a + step * (cnt - 1) + 1 : a;
+        b = min(b, a + step * cnt);
+        a = na;
+    }
+    const uint64_t i = a + (uint64_t)lane;
+    return a + (uint64_t)__builtin_popcountll(__ballot(i < b && key(i) <= x));
+}
+
 // Inclusive tail of the 1 KiB chunk starting at p (warm-up only; p may lie
 // before glo or even before the buffer: those bytes read as invalid).
 template <int K>
@@ -277,13 +296,9 @@ __device__ __noinline__ uint32_t chunk_tail(const uint8_t* bytes, const uint64_t
     const int64_t b0 = p + 16 * lane;
     uint4 d = make_uint4(0u, 0u, 0u, 0u);
     if (b0 >= (int64_t)(glo & ~(uint64_t)15)) d = *(const uint4*)(A.bytes + b0);
-    // first excluded interval that ends after the chunk start (binary search)
+    // first excluded interval that ends after the chunk start
     const uint64_t key = p < 0 ? 0 : (uint64_t)p;
-    uint64_t lo = 0, hi = A.n_excl;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (A.excl[2 * mid + 1] <= key) lo = mid + 1; else hi = mid;
-    }
+    const uint64_t lo = wave_upper_bound(A.n_excl, key, lane, [&](uint64_t i) { return A.excl[2 * i + 1]; });
     ChunkMask m{glo, 0, 0};
     uint32_t C, V, EN, ne, own;
     front_end<K, true>(d, A, (uint64_t)p, lane, m, lo, C, V, EN, ne, own);
@@ -311,12 +326,25 @@ struct Range {
     __device__ __forceinline__ uint32_t rel_of(uint64_t x) const {
         return x <= c0 ? 0u : (x - c0 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(x - c0));
     }
-    // requires lo < hi
+    // Addresses only (no loads), so the chunk stream can be put in flight before
+    // the warm-up's dependent loads.  Requires lo < hi.
+    __device__ __forceinline__ void init(uint64_t glo_, uint64_t ghi_, uint64_t lo_, uint64_t hi_) {
+        glo = glo_, ghi = ghi_, lo = lo_, hi = hi_;
+        c0 = lo & ~(uint64_t)15;
+        lo_r = (uint32_t)(lo - c0);
+        hi_r = (uint32_t)(hi - c0);
+        end_r = rel_of((ghi + 15) & ~(uint64_t)15);
+        nch = (hi_r + kChunk - 1) / kChunk;
+    }
     template <int K>
     __device__ __forceinline__ void begin(const CountArgs& A, uint64_t glo_, uint64_t ghi_, uint64_t lo_,
                                           uint64_t hi_, int lane) {
-        glo = glo_, ghi = ghi_, lo = lo_, hi = hi_;
-        c0 = lo & ~(uint64_t)15;
+        init(glo_, ghi_, lo_, hi_);
+        warm<K>(A, lane);
+    }
+    // Context and first interval (after init).
+    template <int K>
+    __device__ __forceinline__ void warm(const CountArgs& A, int lane) {
         // warm-up: exact k-1 context before c0 (walk back until complete)
         carry = tail_pack(0, 0, 0);
         for (int64_t p = (int64_t)c0; p > (int64_t)glo && !tail_complete<K>(carry);) {
@@ -326,21 +354,12 @@ struct Range {
         // first excluded interval ending after c0; its bounds live in registers so
         // the chunk loop issues no vector loads besides the byte stream (a VMEM load
         // there would force vmcnt(0) and drain the prefetch ring)
-        uint64_t a = 0, b = A.n_excl;
-        while (a < b) {
-            const uint64_t mid = (a + b) >> 1;
-            if (uload64(A.excl + 2 * mid + 1) <= c0) a = mid + 1; else b = mid;
-        }
-        iv = a;
+        iv = wave_upper_bound(A.n_excl, c0, lane, [&](uint64_t i) { return A.excl[2 * i + 1]; });
         ivs_r = ive_r = 0xFFFFFFFFu;
         if (iv < A.n_excl) {
             ivs_r = rel_of(uload64(A.excl + 2 * iv));
             ive_r = rel_of(uload64(A.excl + 2 * iv + 1));
         }
-        lo_r = (uint32_t)(lo - c0);
-        hi_r = (uint32_t)(hi - c0);
-        end_r = rel_of((ghi + 15) & ~(uint64_t)15);
-        nch = (hi_r + kChunk - 1) / kChunk;
     }
     // true if the chunk at rel needs the masked path (range edge or an excluded
     // interval inside); advances the interval pointer past finished intervals
