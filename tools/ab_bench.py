@@ -42,12 +42,14 @@ def main():
             kc.count(db, cnt, tot)  # warm (also selects/caches the variant's grid)
             torch.cuda.synchronize()
             evs = []
+            zero_first = args.k <= 8   # as bench.py: k >= 9 (bucket kernels) write rows whole
             for _ in range(args.reps):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                cnt.zero_()
-                tot.zero_()
+                if zero_first:
+                    cnt.zero_()
+                    tot.zero_()
                 a.record()
-                kc.count(db, cnt, tot, accumulate=True)
+                kc.count(db, cnt, tot, accumulate=zero_first)
                 b.record()
                 evs.append((a, b))
             torch.cuda.synchronize()
