@@ -27,6 +27,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
 import sys
 import time
 
@@ -64,9 +65,45 @@ def cpu_baseline(args, ids: list[int]) -> dict:
         if el >= args.cpu_seconds or passes >= 1000:
             break
     bases = n * args.seq_len * passes
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": round(bases / el / 1e9, 4), "unit": "Gbases/s", "cores": threads, "kind": "port",
+            "host": {"nproc": os.cpu_count(), "cpu": cpu, "jellyfish_on_path": bool(shutil.which("jellyfish"))},
             "sample": f"{n} synthetic {args.seq_len // 10**6} Mbp genomes x {passes} passes "
                       f"({el:.1f} s, oracle/kmer_oracle.c OpenMP, k={args.k})"}
+
+
+def stream_ceiling(torch, data, stream) -> dict:
+    """Practical HBM ceilings on this device, measured on the resident batch:
+    a device-to-device copy (read + write bytes / time) and a read-only
+    reduction (SURVEY section 8(d) asks for a measured ceiling beside the spec peak)."""
+    n = (data.numel() // 16) * 16
+    src = data[:n]
+    dst = torch.empty_like(src)
+    words = src.view(torch.int32)
+
+    def timed(fn, reps=5):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            fn()
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps * 1e-3
+
+    t_copy = timed(lambda: dst.copy_(src))
+    t_read = timed(lambda: words.sum(dtype=torch.int64))
+    del dst
+    return {"d2d_copy_GBps": round(2 * n / t_copy / 1e9, 1), "read_reduce_GBps": round(n / t_read / 1e9, 1),
+            "bytes": int(n)}
 
 
 def load_traffic(k: int, workload_tag: str):
@@ -189,6 +226,7 @@ def main() -> None:
         return ok
 
     kc, counts, totals, el, kern_ms = run(args.k, args.steps, args.warmup)
+    ceiling = stream_ceiling(torch, db.data, stream) if rank == 0 else None
     alg_bytes = fasta_bytes + 4 * kc.nbins * n          # per launch
     ok = verify(args.k, counts, totals)
     grid, block, lds = kc.launch_info()
@@ -218,7 +256,8 @@ def main() -> None:
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": int(alg_bytes)},
+                     "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": int(alg_bytes),
+                     "measured_ceiling": ceiling},
         "parity": "ok" if ok else "MISMATCH",
     }
     if args.secondary_k and world == 1 and args.secondary_k != args.k:
