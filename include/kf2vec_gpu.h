@@ -110,6 +110,11 @@ int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_gen
  * threads per workgroup, dynamic LDS bytes); for roofline accounting. */
 int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
 
+/* Measurement aid (bench.py): read d_bytes[0, n) with the count kernel's access
+ * pattern and XOR-fold it into *d_out (device).  Time it to get the practical
+ * HBM read ceiling of that pattern.  Needs n rounded up to 16 readable. */
+int kf_stream_probe(const uint8_t* d_bytes, uint64_t n, uint32_t* d_out, void* stream);
+
 /* Free the large-k workspace and tables of the current device (synchronises the
  * device).  The next large-k kf_count_batch allocates them again. */
 int kf_workspace_release(void);

@@ -39,6 +39,7 @@ SIGNATURES = {
     "kf_count_batch": (_int, [_vp, _vp, _i32, _vp, _u64, _vp, _vp, _int, _vp, _vp, _u32, _vp]),
     "kf_count_launch_info": (_int, [_int, _PI, _PI, _PI]),
     "kf_workspace_release": (_int, []),
+    "kf_stream_probe": (_int, [_vp, _u64, _vp, _vp]),
     "kf_synth_fasta": (_int, [_vp, _vp, _i32, _i64, _i64, _u64, _u64, _int, _u64, _vp]),
     "kf_synth_genome_bytes": (_u64, [_i64, _u64, _int, _u64]),
     "kf_synth_header_len": (_u64, [_i64]),

@@ -421,6 +421,41 @@ __global__ void __launch_bounds__(256) synth_kernel(uint8_t* bytes, const uint64
     }
 }
 
+// ---------------------------------------------------------------- stream probe
+// Reads a byte range with the count kernel's access pattern (per wave a
+// contiguous range, 1 KiB chunks, 16 B per lane, 6-deep buffer-load ring) and
+// XOR-folds it: the practical HBM read ceiling for this pattern (bench.py).
+__global__ void __launch_bounds__(1024) stream_probe_kernel(const uint8_t* bytes, uint64_t n, uint32_t* out) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / kWave);
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6);
+    // whole 1 KiB chunks per wave (the last one clamped to n by the descriptor)
+    const uint64_t nck = (n + kChunk - 1) / kChunk;
+    const uint64_t lo = min(n, (nck * w / nw) * kChunk), hi = min(n, (nck * (w + 1) / nw) * kChunk);
+    uint32_t acc = 0;
+    if (lo < hi) {
+        Range rg;
+        rg.init(0, n, lo, hi);
+        constexpr int RING = 6;
+        uint4 buf[RING];
+#pragma unroll
+        for (int j = 0; j < RING; ++j) buf[j] = rg.load(bytes, j * kChunk, lane);
+        uint32_t rel = 0;
+        for (uint32_t i = 0; i + RING <= rg.nch; i += RING) {
+#pragma unroll
+            for (int j = 0; j < RING; ++j) {
+                acc ^= buf[j].x ^ buf[j].y ^ buf[j].z ^ buf[j].w;
+                rel += kChunk;
+                buf[j] = rg.load(bytes, rel + (RING - 1) * kChunk, lane);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RING - 1; ++j)
+            if (rg.nch % RING > (uint32_t)j) acc ^= buf[j].x ^ buf[j].y ^ buf[j].z ^ buf[j].w;
+    }
+    if (acc) atomicXor(out, acc);
+}
+
 }  // namespace kf
 
 // ====================================================================== C-ABI
@@ -581,6 +616,20 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
                 fprintf(stderr, "  wave %2d: %.0f cyc/chunk over %llu chunks\n", w, (double)h[8 + w] / h[24 + w],
                         h[24 + w]);
     }
+    return KF_OK;
+}
+
+extern "C" int kf_stream_probe(const uint8_t* d_bytes, uint64_t n, uint32_t* d_out, void* stream) {
+    if (!d_bytes || !d_out) return kf_fail(KF_EINVAL, "null device pointer");
+    if (((uintptr_t)d_bytes) & 15) return kf_fail(KF_EINVAL, "d_bytes must be 16-byte aligned");
+    if (n == 0) return KF_OK;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return kf_fail(KF_EHIP, "device query failed");
+    hipLaunchKernelGGL(stream_probe_kernel, dim3(2 * (cus > 0 ? cus : 1)), dim3(1024), 0, (hipStream_t)stream,
+                       d_bytes, n, d_out);
+    if (hipGetLastError() != hipSuccess) return kf_fail(KF_EHIP, "stream probe launch failed");
     return KF_OK;
 }
 

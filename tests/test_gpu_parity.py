@@ -300,3 +300,17 @@ def test_count_kernel_variants_match_oracle(torch_dev, oracle, monkeypatch, vari
                               crlf_rate=0.05) for _ in range(20)]
     counts, totals = run_batch(blobs, k, torch_dev)
     check_against_oracle(oracle, blobs, k, counts, totals, tag=f"v{variant}")
+
+
+def test_stream_probe_xor_fold(torch_dev):
+    """kf_stream_probe (bench.py's read-ceiling probe) reads every byte exactly once."""
+    import torch
+    from kf2vecfsw_amd import _native as N
+    rng = np.random.default_rng(5)
+    for n in (16, 1024, 1040, 5_000_000, 12_345_680):
+        host = rng.integers(0, 2 ** 32, size=n // 4, dtype=np.uint64).astype(np.uint32)
+        d = torch.from_numpy(host.view(np.int32)).to(torch_dev).view(torch.uint8)
+        out = torch.zeros(1, dtype=torch.int32, device=torch_dev)
+        N.check(N.lib().kf_stream_probe(d.data_ptr(), n, out.data_ptr(), None), "kf_stream_probe")
+        torch.cuda.synchronize()
+        assert int(out.cpu().numpy().view(np.uint32)[0]) == int(np.bitwise_xor.reduce(host)), n
