@@ -147,10 +147,18 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob: KF_BENCH_REHEARSE=1 runs every rank on cuda:0 over gloo (one
+    # GPU box); the real multi-GPU run uses one GPU per rank over RCCL
+    rehearse = os.environ.get("KF_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -253,7 +261,9 @@ def main() -> None:
         "dtype": "u32",
         "data": "synthetic (device-generated, seeded splitmix64; no datasets)",
         "config": {"workload": f"{'1' if world == 1 else world}xMI355X, k={args.k}, {n} synthetic "
-                               f"{args.seq_len / 1e6:g} Mbp genomes per GPU (BASELINE configs[1])",
+                               f"{args.seq_len / 1e6:g} Mbp genomes per GPU "
+                               + ("(BASELINE configs[1])" if world == 1 else
+                                  "(BASELINE configs[3] scaling curve, weak: fixed batch per GPU)"),
                    "k": args.k, "genomes_per_gpu": n, "seq_len": args.seq_len, "line_width": 80,
                    "global_batch": n * world, "parallelism": f"round-robin genome shards x{world}, no collective",
                    "kernel_grid": [grid, block], "lds_bytes": lds},
