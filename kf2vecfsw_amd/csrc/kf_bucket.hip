@@ -46,12 +46,18 @@ constexpr uint64_t kRecCap = (uint64_t)kRmax * kRoundRecs;   // u16 records per 
 template <int K>
 struct Bk {
     static constexpr uint32_t nbk = (1u << (2 * K)) >> kBkBits;   // buckets
-    // LDS byte layout: histogram / round staging at 0, then counters
-    static constexpr uint32_t hist = 0;                            // 128 KiB (stage: first 32 KiB)
-    static constexpr uint32_t cnt = kBkCodes * 4;                  // nbk u32: round rank counters
-    static constexpr uint32_t rbase = cnt + nbk * 4;               // nbk+1 u32: round bucket offsets
-    static constexpr uint32_t red = (rbase + (nbk + 1) * 4 + 7) & ~7u;   // kBkWaves u64
+    // LDS byte layout.  Phase 2: the 128 KiB histogram at 0.  Phase 1 reuses it:
+    // two 32 KiB round staging buffers at 0 and 32 KiB, then one private
+    // bucket-offset table per wave at 64 KiB.  After it: three rotating sets of
+    // round rank counters, and the reduction slots.
+    static constexpr uint32_t hist = 0;
+    static constexpr uint32_t stage = 0;                            // + (r & 1) * kStageBytes
+    static constexpr uint32_t rbase = 2 * 32768;                    // + wave * (nbk + 1) * 4
+    static constexpr uint32_t dirty = rbase + kBkWaves * (nbk + 1) * 4;   // phase-1 footprint in hist
+    static constexpr uint32_t cnt = kBkCodes * 4;                   // + (r % 3) * nbk * 4
+    static constexpr uint32_t red = (cnt + 3 * nbk * 4 + 7) & ~7u;  // kBkWaves u64
     static constexpr uint32_t lds_bytes = red + kBkWaves * 8;
+    static_assert(dirty <= kBkCodes * 4, "phase-1 tables must fit the histogram area");
 };
 
 struct BucketArgs {
@@ -193,9 +199,29 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             buf[j] = (uint32_t)j < nch ? rg.load(A.bytes, j * kChunk, lane) : make_uint4(0u, 0u, 0u, 0u);
         if (lo < hi) rg.warm<K>(A, lane);
         uint32_t carry = lo < hi ? rg.carry : 0u;
-        uint32_t off = 0;   // records written so far (multiple of 8)
         uint32_t rel = 0;
+        // One barrier per round.  Round r: zero the counter set of round r+1,
+        // count + rank this round's records in set r % 3, barrier; then copy out
+        // round r-1 (staged in the other buffer before this barrier), every wave
+        // computes the bucket offsets of round r into its private table (no
+        // serial scan, no second barrier), and stages its records.  A counter set
+        // is zeroed two rounds after its last read, so the barriers order it.
+        for (uint32_t i = tid; i < 3 * NBK; i += kBkBlock) lds_st(L::cnt + 4 * i, 0u);
+        lds_barrier();
+        uint32_t off = 0;                    // records of rounds before the current one (x8)
+        uint32_t t_prev = 0, off_prev = 0;   // last staged round, copied out one round later
+        const uint32_t rb = L::rbase + (uint32_t)wave * (NBK + 1) * 4;
+        auto copy_out = [&](uint32_t r, uint32_t T, uint32_t o) {
+            const uint32_t st = L::stage + (r & 1) * 32768;
+            for (uint32_t q = tid; q < (T + 7) / 8; q += kBkBlock) {
+                const v4u v = *(lds_v4u*)(uintptr_t)(st + 16 * q);
+                *(v4u*)(rec + o + 8 * q) = v;
+            }
+        };
         auto round = [&](uint32_t r, uint4& bf) {
+            const uint32_t cb = L::cnt + 4 * NBK * (r % 3);
+            const uint32_t cz = L::cnt + 4 * NBK * ((r + 1) % 3);
+            for (uint32_t b = tid; b < NBK; b += kBkBlock) lds_st(cz + 4 * b, 0u);
             uint32_t s[16], rk[16];
             const bool have = r < nch;
             if (have) {
@@ -212,65 +238,55 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                 canon_std<K>(w, s);
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
-                    if (s[j] != 0xFFFFFFFFu) rk[j] = lds_add_rtn(L::cnt + ((s[j] >> kBkBits) << 2), 1u);
+                    if (s[j] != 0xFFFFFFFFu) rk[j] = lds_add_rtn(cb + ((s[j] >> kBkBits) << 2), 1u);
                 rel += kChunk;
                 if (rel + 3 * kChunk < nch * kChunk) bf = rg.load(A.bytes, rel + 3 * kChunk, lane);
             }
             lds_barrier();
-            // bucket offsets of this round (wave 0), counters reset for the next
-            if (wave == 0) {
-                constexpr uint32_t PER = (NBK + kWave - 1) / kWave;
-                uint32_t loc[PER];
-                uint32_t sum = 0;
+            if (r > 0) copy_out(r - 1, t_prev, off_prev);
+            // bucket offsets of round r (exclusive prefix over buckets), per wave
+            constexpr uint32_t PER = (NBK + kWave - 1) / kWave;
+            uint32_t loc[PER];
+            uint32_t sum = 0;
 #pragma unroll
-                for (uint32_t j = 0; j < PER; ++j) {
-                    const uint32_t b = (uint32_t)lane * PER + j;
-                    uint32_t v = 0;
-                    if (b < NBK) {
-                        v = lds_ld(L::cnt + 4 * b);
-                        lds_st(L::cnt + 4 * b, 0u);
-                    }
-                    loc[j] = sum;
-                    sum += v;
-                }
-                uint32_t inc = sum;
+            for (uint32_t j = 0; j < PER; ++j) {
+                const uint32_t b = (uint32_t)lane * PER + j;
+                const uint32_t v = b < NBK ? lds_ld(cb + 4 * b) : 0u;
+                loc[j] = sum;
+                sum += v;
+            }
+            uint32_t inc = sum;
 #pragma unroll
-                for (int d = 1; d < kWave; d <<= 1) {
-                    const uint32_t o = __shfl_up(inc, d, kWave);
-                    if (lane >= d) inc += o;
-                }
-                const uint32_t ex = inc - sum;
+            for (int d = 1; d < kWave; d <<= 1) {
+                const uint32_t o = __shfl_up(inc, d, kWave);
+                if (lane >= d) inc += o;
+            }
+            const uint32_t ex = inc - sum;
+            const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
 #pragma unroll
-                for (uint32_t j = 0; j < PER; ++j) {
-                    const uint32_t b = (uint32_t)lane * PER + j;
-                    if (b < NBK) {
-                        lds_st(L::rbase + 4 * b, ex + loc[j]);
-                        meta[(uint64_t)b * kRmax + r] = (uint16_t)(ex + loc[j]);
-                    }
-                }
-                if (lane == kWave - 1) {
-                    lds_st(L::rbase + 4 * NBK, inc);
-                    meta[(uint64_t)NBK * kRmax + r] = (uint16_t)inc;
-                    roff[r] = off;
+            for (uint32_t j = 0; j < PER; ++j) {
+                const uint32_t b = (uint32_t)lane * PER + j;
+                if (b < NBK) {
+                    lds_st(rb + 4 * b, ex + loc[j]);
+                    if (wave == 0) meta[(uint64_t)b * kRmax + r] = (uint16_t)(ex + loc[j]);
                 }
             }
-            lds_barrier();
+            if (wave == 0 && lane == kWave - 1) {
+                meta[(uint64_t)NBK * kRmax + r] = (uint16_t)T;
+                roff[r] = off;
+            }
             if (have) {
+                const uint32_t st = L::stage + (r & 1) * 32768;
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     if (s[j] != 0xFFFFFFFFu) {
-                        const uint32_t slot = lds_ld(L::rbase + ((s[j] >> kBkBits) << 2)) + rk[j];
-                        *(volatile lds_u16*)(uintptr_t)(L::hist + 2 * slot) = (uint16_t)(s[j] & (kBkCodes - 1));
+                        const uint32_t slot = lds_ld(rb + ((s[j] >> kBkBits) << 2)) + rk[j];
+                        *(volatile lds_u16*)(uintptr_t)(st + 2 * slot) = (uint16_t)(s[j] & (kBkCodes - 1));
                     }
                 }
             }
-            const uint32_t T = lds_ld(L::rbase + 4 * NBK);
-            lds_barrier();
-            // copy the sorted round out, 16 B per lane
-            for (uint32_t q = tid; q < (T + 7) / 8; q += kBkBlock) {
-                const v4u v = *(lds_v4u*)(uintptr_t)(L::hist + 16 * q);
-                *(v4u*)(rec + off + 8 * q) = v;
-            }
+            t_prev = T;
+            off_prev = off;
             off += (T + 7) & ~7u;
         };
         uint32_t r = 0;
@@ -283,13 +299,15 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         if (r < nround) round(r++, buf[0]);
         if (r < nround) round(r++, buf[1]);
         if (r < nround) round(r++, buf[2]);
+        lds_barrier();
+        if (nround > 0) copy_out(nround - 1, t_prev, off_prev);
 
         // ---------------------------------------------------------- phase 2
         // records and meta were stored by other waves of this workgroup: wait for
         // the stores, and read them with L1-bypassing loads below
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         const uint64_t t_p2 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
-        for (uint32_t i = tid; i < kRoundRecs / 2; i += kBkBlock) lds_st(L::hist + 4 * i, 0u);   // staging area
+        for (uint32_t i = tid; i < L::dirty / 4; i += kBkBlock) lds_st(L::hist + 4 * i, 0u);   // phase-1 area
         lds_barrier();
         uint32_t* row = A.counts + (uint64_t)g * A.nbins;
         const bool split = np > 1;
@@ -439,7 +457,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             for (int x = 0; x < kFG; ++x) flush_cols((c0 & ~3u) + 4 * ((uint32_t)tid + x * kBkBlock), ci[x], c0, c1);
             for (uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + kFG * kBkBlock); g4 < c1; g4 += 4 * kBkBlock)
                 flush_cols(g4, *(const v2u*)(B.col_idx + g4), c0, c1);
-            if (B.prof) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[2] += t - t0; t0 = t; }
+            if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[2] += t - t0; t0 = t; }
             lds_barrier();
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[3] += t - t0; }
         }
