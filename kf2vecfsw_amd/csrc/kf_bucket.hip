@@ -559,6 +559,17 @@ int ensure_tables(DevState& d, int k) {
 
 namespace kf {
 
+int bucket_launch_info(int k, int* grid, int* block, int* lds) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return kf_fail(KF_EHIP, "device query failed");
+    *grid = cus > 0 ? cus : 1;
+    *block = kBkBlock;
+    *lds = (int)bucket_lds_for(k);
+    return KF_OK;
+}
+
 int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
@@ -569,7 +580,7 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     DevState& d = g_dev[dev];
     int rc = ensure_tables(d, k);
     if (rc) return rc;
-    const uint32_t lds = bucket_lds_for(k), nbk = (1u << (2 * k)) >> kBkBits;
+    const uint32_t lds = bucket_lds_for(k);
     if (!d.grid) {
         if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
@@ -617,7 +628,6 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     B.roff = (uint32_t*)((char*)d.scratch + rec_b + meta_b);
     B.accumulate = (flags & KF_ACCUMULATE) ? 1u : 0u;
     B.prof = nullptr;
-    (void)nbk;
     const char* pe = getenv("KF_BUCKET_PROFILE");   // debugging aid: synchronous, prints to stderr
     std::vector<unsigned long long> prof_h;
     if (pe && *pe == '1') {

@@ -555,6 +555,7 @@ int launch_info(int k, int* grid, int* block, int* lds, int* variant) {
 extern "C" int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes) {
     if (k < KF_MIN_K || k > KF_MAX_K) return kf_fail(KF_EINVAL, "k out of range [2, 12]");
     if (!grid || !block || !lds_bytes) return kf_fail(KF_EINVAL, "null output pointer");
+    if (k >= bucket_min_k()) return bucket_launch_info(k, grid, block, lds_bytes);
     int v = 0;
     return launch_info(k, grid, block, lds_bytes, &v);
 }

@@ -431,5 +431,6 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // Large k: two-phase LDS bucket counting (kf_bucket.hip).  Count rows are
 // written whole (no memset needed unless accumulating); the caller zeroes totals.
 int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s);
+int bucket_launch_info(int k, int* grid, int* block, int* lds);
 
 }  // namespace kf
