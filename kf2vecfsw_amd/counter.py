@@ -229,6 +229,29 @@ def counts_to_numpy(counts: torch.Tensor) -> np.ndarray:
     return counts.cpu().numpy().view(np.uint32)
 
 
+def features(counts: torch.Tensor, pseudocount: bool = False, raw_cnt: bool = False,
+             scaler: float = 1.0) -> torch.Tensor:
+    """In-memory hand-off: the float64 feature matrix the
+    trainers build from `.kf` files -- `my_read_csv` (utils.py:436-437) then
+    `* features_scaler` (train_classifier_model.py:148, train_model_set.py:291) --
+    computed on the device from the count matrix, without the text round trip.
+
+    Bit-identical to parsing the `.kf` text: the values are main.py:332-342
+    (`+0.5` pseudocount, `v / v.sum()` unless raw) in float64; the row sums are
+    exact (integers or halves below 2^53), each quotient is correctly rounded,
+    and `repr` text round-trips float64 exactly.  An empty genome gives NaN
+    rows, as the reference's "nan" strings parse.
+    """
+    c = counts.to(torch.int64)
+    c = torch.where(c < 0, c + (1 << 32), c)          # uint32 bit patterns held in int32
+    v = c.to(torch.float64)
+    if pseudocount:
+        v = v + 0.5
+    if not raw_cnt:
+        v = v / v.sum(dim=1, keepdim=True)
+    return v * scaler if scaler != 1.0 else v
+
+
 def synth_ids(n: int, g0: int = 0, g_stride: int = 1) -> list[int]:
     return [g0 + i * g_stride for i in range(n)]
 

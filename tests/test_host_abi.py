@@ -168,3 +168,21 @@ def test_get_kmers_matrix_matches_reference_restatement(native, oracle):
         shuf = oracle.kmers_matrix_from_dump([lines[i] for i in rng.permutation(len(lines))], k)
         key = lambda m: m[np.lexsort(m[:, ::-1].T)]
         assert np.array_equal(key(got), key(shuf))
+
+
+@pytest.mark.parametrize("pseudo", [False, True])
+@pytest.mark.parametrize("raw", [False, True])
+def test_features_handoff_equals_kf_text_round_trip(native, pseudo, raw):
+    """counter.features (in-memory hand-off) == parsing the `.kf` line the writer
+    produces, times the trainers' scaler: bit for bit (CPU torch)."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    from kf2vecfsw_amd.main import format_kf
+    rng = np.random.default_rng(21)
+    rows = np.stack([rng.integers(0, 300, size=2080), (rng.pareto(1.0, size=2080) * 10).astype(np.int64),
+                     np.zeros(2080, np.int64), np.full(2080, 2 ** 32 - 7)]).astype(np.uint32)
+    got = C.features(torch.from_numpy(rows.view(np.int32)), pseudo, raw, scaler=10000.0).numpy()
+    for i, r in enumerate(rows):
+        vals = format_kf("s", r, pseudo, raw).decode().rstrip("\n").split(",")[1:]
+        exp = np.array([float(x) for x in vals]) * 10000.0
+        assert np.array_equal(got[i], exp, equal_nan=True), i
