@@ -314,3 +314,21 @@ def test_stream_probe_xor_fold(torch_dev):
         N.check(N.lib().kf_stream_probe(d.data_ptr(), n, out.data_ptr(), None), "kf_stream_probe")
         torch.cuda.synchronize()
         assert int(out.cpu().numpy().view(np.uint32)[0]) == int(np.bitwise_xor.reduce(host)), n
+
+
+@pytest.mark.parametrize("k", [4, 7, 11])
+def test_arbitrary_byte_values(torch_dev, oracle, k):
+    """Byte soup over all 256 values (high-bit bytes, control bytes, '>' and '@'
+    anywhere) mixed into ACGT/acgt runs: classification must match the oracle."""
+    rng = np.random.default_rng(900 + k)
+    alphabet = np.frombuffer(b"ACGTACGTACGTacgtACGT\n\n", np.uint8)
+    blobs = []
+    for t in range(30):
+        n = int(rng.integers(1, 60000))
+        a = alphabet[rng.integers(0, alphabet.size, size=n)]
+        noise = rng.random(n) < (0.001 if t % 2 else 0.05)
+        a[noise] = rng.integers(0, 256, size=int(noise.sum()), dtype=np.uint8)
+        head = b">g\n" if t % 3 else b""
+        blobs.append(head + a.tobytes())
+    counts, totals = run_batch(blobs, k, torch_dev, fmt=1)
+    check_against_oracle(oracle, blobs, k, counts, totals, fmt=1, tag="bytes")
