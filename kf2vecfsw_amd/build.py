@@ -50,6 +50,7 @@ def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
         o = os.path.join(BUILD, s + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
                "-c", os.path.join(CSRC, s), "-o", o] + (["-DKF_ABLATION"] if ablation else [])
+        cmd += os.environ.get("KF_HIPCC_FLAGS", "").split()   # tools/ only (profiling ablations)
         if verbose:
             cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
         subprocess.run(cmd, check=True)

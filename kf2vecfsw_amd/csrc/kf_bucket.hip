@@ -33,6 +33,13 @@
 
 namespace kf {
 
+// Profiling-only ablations (tools/build_abl.sh -DKF_BK_ABL=n; counts are wrong):
+// 1 = no col_idx table reads in the flush, 2 = no record reads in phase 2
+// (hashed stand-ins).
+#ifndef KF_BK_ABL
+#define KF_BK_ABL 0
+#endif
+
 constexpr int kBkBits = 15;                          // 32768 codes per bucket
 constexpr uint32_t kBkCodes = 1u << kBkBits;
 constexpr int kBkWaves = 16;
@@ -41,30 +48,38 @@ constexpr uint32_t kRoundRecs = kBkWaves * kChunk;   // windows per round (<= 16
 constexpr uint64_t kPieceMax = 8ull << 20;           // bytes per piece (one workgroup)
 // rounds per piece: a wave range is <= piece/16 + 16 bytes, i.e. <= 513 chunks
 constexpr uint32_t kRmax = (uint32_t)(kPieceMax / kRoundRecs) + 2;
-constexpr uint64_t kRecCap = (uint64_t)kRmax * kRoundRecs;   // u16 records per workgroup
+// A record is s & 0x7FFF.  Runs (one bucket, one round) are padded to whole
+// 8-record units with sentinels 0x8000 | x, which phase 2 counts into a trash
+// area past the histogram, so a 16-byte unit never needs a range test.
+constexpr uint32_t kSentinel = 0x8000u;
 
 template <int K>
 struct Bk {
     static constexpr uint32_t nbk = (1u << (2 * K)) >> kBkBits;   // buckets
+    static constexpr uint32_t round_cap = kRoundRecs + 7 * nbk;     // records of a padded round
+    static constexpr uint64_t rec_cap = (uint64_t)kRmax * round_cap + 8;   // per workgroup
     // LDS byte layout.  Phase 2: the 128 KiB histogram at 0.  Phase 1 reuses it:
-    // two 32 KiB round staging buffers at 0 and 32 KiB, then one private
-    // bucket-offset table per wave at 64 KiB.  After it: three rotating sets of
-    // round rank counters, and the reduction slots.
+    // two round staging buffers, then one private bucket-offset table per wave.
+    // After the histogram: three rotating sets of round rank counters (phase 1),
+    // which phase 2 reuses as the sentinels' trash bins, and the reduction slots.
     static constexpr uint32_t hist = 0;
-    static constexpr uint32_t stage = 0;                            // + (r & 1) * kStageBytes
-    static constexpr uint32_t rbase = 2 * 32768;                    // + wave * (nbk + 1) * 4
+    static constexpr uint32_t stage_bytes = (round_cap * 2 + 15) & ~15u;
+    static constexpr uint32_t stage = 0;                            // + (r & 1) * stage_bytes
+    static constexpr uint32_t rbase = 2 * stage_bytes;              // + wave * (nbk + 1) * 4
     static constexpr uint32_t dirty = rbase + kBkWaves * (nbk + 1) * 4;   // phase-1 footprint in hist
     static constexpr uint32_t cnt = kBkCodes * 4;                   // + (r % 3) * nbk * 4
     static constexpr uint32_t red = (cnt + 3 * nbk * 4 + 7) & ~7u;  // kBkWaves u64
-    static constexpr uint32_t lds_bytes = red + kBkWaves * 8;
+    static constexpr uint32_t lds_bytes =
+        red + kBkWaves * 8 > cnt + 256 ? red + kBkWaves * 8 : cnt + 256;   // trash: 64 bins at cnt
     static_assert(dirty <= kBkCodes * 4, "phase-1 tables must fit the histogram area");
+    static_assert(round_cap < 65536, "round offsets are u16");
 };
 
 struct BucketArgs {
     const uint16_t* col_idx;   // nbins: canonical code & 0x7FFF per column
     const uint32_t* bcol;      // nbk+1: first column of each bucket
     const uint32_t* pstart;    // n_genomes+1: first piece of each genome
-    uint16_t* rec;             // gridDim.x * kRecCap records
+    uint16_t* rec;             // gridDim.x * Bk<K>::rec_cap records
     uint16_t* meta;            // gridDim.x * (nbk+1) * kRmax round bucket offsets
     uint32_t* roff;            // gridDim.x * kRmax round record offsets
     uint32_t accumulate;
@@ -165,7 +180,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
     for (uint32_t i = tid; i < kBkCodes + NBK; i += kBkBlock) lds[i] = 0;   // histogram + counters
     __syncthreads();
 
-    uint16_t* rec = B.rec + (uint64_t)blockIdx.x * kRecCap;
+    uint16_t* rec = B.rec + (uint64_t)blockIdx.x * L::rec_cap;
     uint16_t* meta = B.meta + (uint64_t)blockIdx.x * (NBK + 1) * kRmax;
     uint32_t* roff = B.roff + (uint64_t)blockIdx.x * kRmax;
     const uint32_t npiece = B.pstart[A.n_genomes];
@@ -212,8 +227,8 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         uint32_t t_prev = 0, off_prev = 0;   // last staged round, copied out one round later
         const uint32_t rb = L::rbase + (uint32_t)wave * (NBK + 1) * 4;
         auto copy_out = [&](uint32_t r, uint32_t T, uint32_t o) {
-            const uint32_t st = L::stage + (r & 1) * 32768;
-            for (uint32_t q = tid; q < (T + 7) / 8; q += kBkBlock) {
+            const uint32_t st = L::stage + (r & 1) * L::stage_bytes;
+            for (uint32_t q = tid; q < T / 8; q += kBkBlock) {
                 const v4u v = *(lds_v4u*)(uintptr_t)(st + 16 * q);
                 *(v4u*)(rec + o + 8 * q) = v;
             }
@@ -246,21 +261,17 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             if (r > 0) copy_out(r - 1, t_prev, off_prev);
             // bucket offsets of round r (exclusive prefix over buckets), per wave
             constexpr uint32_t PER = (NBK + kWave - 1) / kWave;
-            uint32_t loc[PER];
+            uint32_t loc[PER], cntv[PER];
             uint32_t sum = 0;
 #pragma unroll
             for (uint32_t j = 0; j < PER; ++j) {
                 const uint32_t b = (uint32_t)lane * PER + j;
                 const uint32_t v = b < NBK ? lds_ld(cb + 4 * b) : 0u;
                 loc[j] = sum;
-                sum += v;
+                cntv[j] = v;
+                sum += (v + 7) & ~7u;   // runs padded to whole units
             }
-            uint32_t inc = sum;
-#pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const uint32_t o = __shfl_up(inc, d, kWave);
-                if (lane >= d) inc += o;
-            }
+            const uint32_t inc = wave_incl_scan(sum);
             const uint32_t ex = inc - sum;
             const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
 #pragma unroll
@@ -275,8 +286,21 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                 meta[(uint64_t)NBK * kRmax + r] = (uint16_t)T;
                 roff[r] = off;
             }
+            const uint32_t st = L::stage + (r & 1) * L::stage_bytes;
+            // sentinels after each run, up to its unit boundary (one wave per
+            // round, rotating)
+            if ((r % kBkWaves) == (uint32_t)wave) {
+#pragma unroll
+                for (uint32_t j = 0; j < PER; ++j) {
+                    const uint32_t b = (uint32_t)lane * PER + j;
+                    const uint32_t e = ex + loc[j] + cntv[j], npad = (8u - (cntv[j] & 7u)) & 7u;
+#pragma unroll
+                    for (uint32_t x = 0; x < 7; ++x)
+                        if (b < NBK && x < npad)
+                            *(volatile lds_u16*)(uintptr_t)(st + 2 * (e + x)) = (uint16_t)(kSentinel | ((e + x) & 63u));
+                }
+            }
             if (have) {
-                const uint32_t st = L::stage + (r & 1) * 32768;
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     if (s[j] != 0xFFFFFFFFu) {
@@ -287,7 +311,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             }
             t_prev = T;
             off_prev = off;
-            off += (T + 7) & ~7u;
+            off += T;
         };
         uint32_t r = 0;
         for (; r + 4 <= nround; r += 4) {
@@ -313,75 +337,82 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         const bool split = np > 1;
         unsigned long long tsum = 0;
         // Run table of this wave: lane j (< nrun) <-> round wave + 16 j.  A run is
-        // the records [s, e) of one bucket in one round; it is read in 8-record
-        // (16-byte) units, and the units of all the wave's runs are laid end to end
-        // (prefix P over lanes) so every load instruction carries 64 full units
-        // whatever the run lengths.  Loads are software-pipelined one group of
-        // 4 x 64 units ahead, across bucket boundaries (the next bucket's first
-        // group is in flight during this bucket's flush).
+        // the whole units of one bucket in one round (padded by phase 1), and the
+        // units of all the wave's runs are laid end to end (prefix P over lanes),
+        // so every load instruction carries 64 units whatever the run lengths.
+        // A group is kGW windows of 64 units (512 units: a whole k=11 bucket of a
+        // wave, typically); the next bucket's first group is issued before this
+        // bucket's flush, so its loads are in flight during the flush.  Loads are
+        // unconditional (inactive lanes read unit 0) so vmcnt stays exact.
         const uint32_t myr = (uint32_t)wave + kBkWaves * (uint32_t)lane;
+        const bool myr_ok = myr < nround;
+        const uint32_t myr_c = myr_ok ? myr : 0u;
         const uint32_t nrun = nround > (uint32_t)wave ? (nround - (uint32_t)wave + kBkWaves - 1) / kBkWaves : 0u;
-        const uint32_t ro = myr < nround ? __builtin_nontemporal_load(roff + myr) : 0u;
+        const uint32_t ro_l = __builtin_nontemporal_load(roff + myr_c);
+        const uint32_t ro = myr_ok ? ro_l : 0u;
+        // raw (lanes without a run read round 0; make_tbl masks them), so that
+        // the load is not waited for until its table is built
         auto meta_at = [&](uint32_t b) -> uint32_t {
-            return myr < nround ? __builtin_nontemporal_load(meta + (uint64_t)b * kRmax + myr) : 0u;
+            return __builtin_nontemporal_load(meta + (uint64_t)b * kRmax + myr_c);
         };
         struct Tbl {
-            uint32_t n, P, D, S, E;   // per lane (run)
-            uint32_t U, jc, w0;       // wave-uniform
+            uint32_t P, DL;          // per lane (run): first unit in the bucket's unit space, unit delta
+            uint32_t U, jn, cur, w0; // wave-uniform
         };
         auto make_tbl = [&](uint32_t rs, uint32_t re) {
             Tbl t;
-            t.n = re > rs ? ((re + 7) >> 3) - (rs >> 3) : 0u;
-            uint32_t inc = t.n;
-#pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const uint32_t o = __shfl_up(inc, d, kWave);
-                if (lane >= d) inc += o;
-            }
-            t.P = inc - t.n;
+            const uint32_t n = myr_ok ? (re - rs) >> 3 : 0u;   // rs, re: 8-aligned
+            const uint32_t inc = wave_incl_scan(n);
+            t.P = inc - n;
             t.U = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-            t.D = ro + 8 * (rs >> 3) - 8 * t.P;   // record index of unit u = D + 8u
-            t.S = ro + rs;                        // counted records [S, E)
-            t.E = ro + re;
-            t.jc = 0;
+            t.DL = ((ro + rs) >> 3) - t.P;   // unit u of the bucket is record unit u + DL
+            t.jn = 0;
+            t.cur = 0;
             t.w0 = 0;
             return t;
         };
+        constexpr int kGW = 8;
         struct Grp {
-            v4u v[4];
-            uint32_t q[4], qs[4], qe[4];
+            v4u v[kGW];
+            uint32_t act;   // bit x: this lane's unit of window x exists
+            uint32_t w0;    // first unit of the group
         };
-        // next 4 windows of 64 units of table t -> loads in flight
+        // next kGW windows of 64 units of table t -> loads in flight
         auto issue = [&](Tbl& t, Grp& G) {
+            G.act = 0;
+            G.w0 = t.w0;
 #pragma unroll
-            for (int x = 0; x < 4; ++x) {
+            for (int x = 0; x < kGW; ++x) {
                 const uint32_t w0 = t.w0 + x * kWave, u = w0 + (uint32_t)lane;
-                uint32_t q = 0, qs = 0, qe = 0;
-                while (t.jc < nrun) {
-                    const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)t.P, (int)t.jc);
-                    const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)t.n, (int)t.jc);
+                uint32_t dl = t.cur;
+                while (t.jn < nrun) {   // runs starting in this window
+                    const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)t.P, (int)t.jn);
                     if (pj >= w0 + kWave) break;
-                    if (u >= pj && u < pj + nj) {
-                        q = (uint32_t)__builtin_amdgcn_readlane((int)t.D, (int)t.jc) + 8 * u;
-                        qs = (uint32_t)__builtin_amdgcn_readlane((int)t.S, (int)t.jc);
-                        qe = (uint32_t)__builtin_amdgcn_readlane((int)t.E, (int)t.jc);
-                    }
-                    if (pj + nj > w0 + kWave) break;   // continues into the next window
-                    ++t.jc;
+                    const uint32_t dj = (uint32_t)__builtin_amdgcn_readlane((int)t.DL, (int)t.jn);
+                    dl = u >= pj ? dj : dl;
+                    t.cur = dj;
+                    ++t.jn;
                 }
-                G.q[x] = q, G.qs[x] = qs, G.qe[x] = qe;
-                G.v[x] = qe > qs ? __builtin_nontemporal_load((const v4u*)(rec + q)) : v4u{0u, 0u, 0u, 0u};
+                const bool a = u < t.U;
+                G.act |= a ? 1u << x : 0u;
+                const uint32_t q = a ? 8 * (u + dl) : 0u;
+                if (KF_BK_ABL == 2) {
+                    const uint32_t h = q * 2654435761u;
+                    G.v[x] = v4u{h, h * 2246822519u, h * 3266489917u, h * 668265263u} & 0x7FFF7FFFu;
+                } else {
+                    G.v[x] = __builtin_nontemporal_load((const v4u*)(rec + q));
+                }
             }
-            t.w0 += 4 * kWave;
+            t.w0 += kGW * kWave;
         };
-        auto consume = [&](const Grp& G) {
+        auto consume = [&](const Grp& G, uint32_t U) {
 #pragma unroll
-            for (int x = 0; x < 4; ++x) {
-                const uint32_t d[4] = {G.v[x].x, G.v[x].y, G.v[x].z, G.v[x].w};
+            for (int x = 0; x < kGW; ++x) {
+                if (G.w0 + x * kWave >= U) break;   // wave-uniform
+                if (G.act & (1u << x)) {
+                    const uint32_t d[4] = {G.v[x].x, G.v[x].y, G.v[x].z, G.v[x].w};
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const uint32_t i = G.q[x] + t;
-                    if (i >= G.qs[x] && i < G.qe[x]) lds_add(((d[t >> 1] >> (16 * (t & 1))) & 0xFFFFu) << 2, 1u);
+                    for (int t = 0; t < 8; ++t) lds_add(((d[t >> 1] >> (16 * (t & 1))) & 0xFFFFu) << 2, 1u);
                 }
             }
         };
@@ -392,12 +423,25 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         // loaded before the barrier.
         constexpr int kFG = 8;
         typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-        auto flush_issue = [&](uint32_t b, v2u (&ci)[kFG]) {
-            const uint32_t c0 = B.bcol[b], c1 = B.bcol[b + 1];
+        auto col_at = [&](uint32_t g4) -> v2u {
+            if (KF_BK_ABL == 1) {
+                const uint32_t x = (2 * g4) & 0x7FFCu;
+                return v2u{x | (x + 1) << 16, (x + 2) | (x + 3) << 16};
+            }
+            return *(const v2u*)(B.col_idx + g4);
+        };
+        // c0, c1: the bucket's column range, loaded here (before the next bucket's
+        // record loads) so the flush does not wait on those.
+        auto flush_issue = [&](uint32_t b, v2u (&ci)[kFG], uint32_t& c0, uint32_t& c1) {
+            typedef __attribute__((address_space(4))) const uint32_t const_u32;   // scalar loads (lgkmcnt)
+            const const_u32* bc = (const const_u32*)(uintptr_t)B.bcol;
+            c0 = bc[b];
+            c1 = bc[b + 1];
 #pragma unroll
             for (int x = 0; x < kFG; ++x) {
                 const uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + x * kBkBlock);
-                ci[x] = g4 < c1 ? *(const v2u*)(B.col_idx + g4) : v2u{0u, 0u};
+                const v2u c = col_at(g4 < c1 ? g4 : 0u);   // unconditional load
+                ci[x] = g4 < c1 ? c : v2u{0u, 0u};
             }
         };
         auto flush_cols = [&](uint32_t g4, const v2u ci, uint32_t c0, uint32_t c1) {
@@ -429,34 +473,37 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
 
         uint32_t re_next = meta_at(1);
         Tbl tb = make_tbl(meta_at(0), re_next);
-        re_next = NBK > 1 ? meta_at(2) : 0u;
-        Grp G0, G1;
+        uint32_t re_cur = re_next;
+        re_next = meta_at(NBK > 1 ? 2 : 1);
+        Grp G0;
         issue(tb, G0);
         uint64_t tp[4] = {0, 0, 0, 0};   // profile: records, barrier, flush, barrier
         for (uint32_t b = 0; b < NBK; ++b) {
             uint64_t t0 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
-            while (tb.w0 < tb.U) {          // more groups in this bucket
-                issue(tb, G1);
-                consume(G0);
-                G0 = G1;
+            consume(G0, tb.U);
+            while (tb.w0 < tb.U) {   // a bucket beyond one group: synchronous groups
+                issue(tb, G0);
+                consume(G0, tb.U);
             }
-            consume(G0);
             v2u ci[kFG];
-            flush_issue(b, ci);
+            // issue order: bucket b+2's run ends, the flush's col_idx, bucket
+            // b+1's records (vmcnt is in order: each is waited for only when used)
+            const uint32_t m = meta_at(b + 3 < NBK ? b + 3 : NBK);
+            uint32_t c0, c1;
+            flush_issue(b, ci, c0, c1);
             if (b + 1 < NBK) {               // next bucket: table, first group in flight
-                const uint32_t rs_next = tb.E - ro;   // this bucket's run ends
-                tb = make_tbl(rs_next, re_next);
-                re_next = b + 2 < NBK ? meta_at(b + 3) : 0u;
+                tb = make_tbl(re_cur, re_next);   // this bucket's run ends start the next
+                re_cur = re_next;
                 issue(tb, G0);
             }
+            re_next = m;
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[0] += t - t0; t0 = t; }
             lds_barrier();
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[1] += t - t0; t0 = t; }
-            const uint32_t c0 = B.bcol[b], c1 = B.bcol[b + 1];
 #pragma unroll
             for (int x = 0; x < kFG; ++x) flush_cols((c0 & ~3u) + 4 * ((uint32_t)tid + x * kBkBlock), ci[x], c0, c1);
             for (uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + kFG * kBkBlock); g4 < c1; g4 += 4 * kBkBlock)
-                flush_cols(g4, *(const v2u*)(B.col_idx + g4), c0, c1);
+                flush_cols(g4, col_at(g4), c0, c1);
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[2] += t - t0; t0 = t; }
             lds_barrier();
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[3] += t - t0; }
@@ -595,7 +642,8 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     }
     const int grid = d.grid;
     // scratch: records, round metadata (sized for the largest k), round offsets
-    const size_t rec_b = (size_t)grid * kRecCap * 2;
+    const size_t nbk = ((size_t)1 << (2 * k)) >> kBkBits;
+    const size_t rec_b = (size_t)grid * ((size_t)kRmax * (kRoundRecs + 7 * nbk) + 8) * 2;   // Bk<k>::rec_cap
     const size_t meta_b = (size_t)grid * (((1u << (2 * KF_MAX_K)) >> kBkBits) + 1) * kRmax * 2;
     const size_t roff_b = (size_t)grid * kRmax * 4;
     const size_t need = rec_b + meta_b + roff_b;

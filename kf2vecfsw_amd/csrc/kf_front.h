@@ -175,6 +175,18 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t old, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
+// Inclusive prefix sum over the wave on the VALU (DPP row shifts and row
+// broadcasts; no LDS traffic, unlike __shfl_up's ds_bpermute).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+
 // Exclusive scan of lane tails with a carry-in (slow path: some lane's block has
 // fewer than k-1 entries and no reset, e.g. very short FASTA lines).
 template <int K>
