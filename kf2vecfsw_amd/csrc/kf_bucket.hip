@@ -223,6 +223,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         // is zeroed two rounds after its last read, so the barriers order it.
         for (uint32_t i = tid; i < 3 * NBK; i += kBkBlock) lds_st(L::cnt + 4 * i, 0u);
         lds_barrier();
+        uint64_t p1w = 0;                    // profile: phase-1 barrier wait of this wave
         uint32_t off = 0;                    // records of rounds before the current one (x8)
         uint32_t t_prev = 0, off_prev = 0;   // last staged round, copied out one round later
         const uint32_t rb = L::rbase + (uint32_t)wave * (NBK + 1) * 4;
@@ -257,7 +258,14 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                 rel += kChunk;
                 if (rel + 3 * kChunk < nch * kChunk) bf = rg.load(A.bytes, rel + 3 * kChunk, lane);
             }
-            lds_barrier();
+            if (B.prof) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const uint64_t t = __builtin_amdgcn_s_memtime();
+                lds_barrier();
+                p1w += __builtin_amdgcn_s_memtime() - t;
+            } else {
+                lds_barrier();
+            }
             if (r > 0) copy_out(r - 1, t_prev, off_prev);
             // bucket offsets of round r (exclusive prefix over buckets), per wave
             constexpr uint32_t PER = (NBK + kWave - 1) / kWave;
@@ -478,6 +486,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         Grp G0;
         issue(tb, G0);
         uint64_t tp[4] = {0, 0, 0, 0};   // profile: records, barrier, flush, barrier
+        uint64_t tcons = 0;              // profile: consume part of records
         for (uint32_t b = 0; b < NBK; ++b) {
             uint64_t t0 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
             consume(G0, tb.U);
@@ -485,6 +494,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                 issue(tb, G0);
                 consume(G0, tb.U);
             }
+            if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tcons += __builtin_amdgcn_s_memtime() - t0; }
             v2u ci[kFG];
             // issue order: bucket b+2's run ends, the flush's col_idx, bucket
             // b+1's records (vmcnt is in order: each is waited for only when used)
@@ -507,6 +517,13 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[2] += t - t0; t0 = t; }
             lds_barrier();
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[3] += t - t0; }
+        }
+        if (B.prof && lane == 0) {   // per wave: records, barrier, phase-1 barrier, consume
+            unsigned long long* pw = B.prof + 8 * gridDim.x + 4 * (kBkWaves * blockIdx.x + wave);
+            pw[0] += tp[0];
+            pw[1] += tp[1];
+            pw[2] += p1w;
+            pw[3] += tcons;
         }
         tsum = wave_sum(tsum);
         unsigned long long* red = (unsigned long long*)((char*)lds + L::red);
@@ -679,8 +696,8 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     const char* pe = getenv("KF_BUCKET_PROFILE");   // debugging aid: synchronous, prints to stderr
     std::vector<unsigned long long> prof_h;
     if (pe && *pe == '1') {
-        if (hipMalloc((void**)&B.prof, (size_t)grid * 8 * 8) != hipSuccess ||
-            hipMemsetAsync(B.prof, 0, (size_t)grid * 8 * 8, s) != hipSuccess)
+        if (hipMalloc((void**)&B.prof, (size_t)grid * (8 + 4 * kBkWaves) * 8) != hipSuccess ||
+            hipMemsetAsync(B.prof, 0, (size_t)grid * (8 + 4 * kBkWaves) * 8, s) != hipSuccess)
             return kf_fail(KF_EHIP, "profile buffer");
     }
     hipLaunchKernelGGL(piece_scan_kernel, dim3(1), dim3(1024), 0, s, A.goff, A.n_genomes, d.pstart);
@@ -692,7 +709,7 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
         return kf_fail(KF_EHIP, "bucket kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (hipEventRecord(d.done, s) != hipSuccess) return kf_fail(KF_EHIP, "hipEventRecord failed");
     if (B.prof) {
-        prof_h.resize((size_t)grid * 8);
+        prof_h.resize((size_t)grid * (8 + 4 * kBkWaves));
         if (hipStreamSynchronize(s) != hipSuccess ||
             hipMemcpy(prof_h.data(), B.prof, prof_h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
             return kf_fail(KF_EHIP, "profile readback");
@@ -704,6 +721,15 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
         fprintf(stderr, "[kf_bucket k=%d] pieces %.0f cycles/piece: phase1 %.3g phase2 %.3g "
                 "(records %.3g, barrier %.3g, flush %.3g, barrier %.3g)\n",
                 k, sum[2], sum[0] / np, sum[1] / np, sum[3] / np, sum[4] / np, sum[5] / np, sum[6] / np);
+        fprintf(stderr, "[kf_bucket k=%d] per wave, cycles per piece:", k);
+        for (int w = 0; w < kBkWaves; ++w) {
+            double v[4] = {0, 0, 0, 0};
+            for (int i = 0; i < grid; ++i)
+                for (int x = 0; x < 4; ++x) v[x] += (double)prof_h[8 * grid + 4 * (kBkWaves * i + w) + x];
+            fprintf(stderr, "\n  w%d records %.3g (consume %.3g) barrier %.3g | phase-1 barrier %.3g", w, v[0] / np,
+                    v[3] / np, v[1] / np, v[2] / np);
+        }
+        fprintf(stderr, "\n");
     }
     return KF_OK;
 }
