@@ -168,11 +168,22 @@ class DeviceBatch:
 
 
 def to_device(hb: HostBatch, device: torch.device | str = "cuda") -> DeviceBatch:
+    """Asynchronous H2D of a batch on the current stream.  The small offset and
+    interval tables are staged through pinned memory too: a copy from pageable
+    memory would block the host until the stream's earlier copies finish."""
     dev = torch.device(device)
     data = hb.data.to(dev, non_blocking=True)
-    off = torch.from_numpy(hb.off.view(np.int64)).to(dev, non_blocking=True)
     ex = hb.excl if hb.excl.size else np.zeros(2, np.uint64)
-    excl = torch.from_numpy(ex.view(np.int64)).to(dev, non_blocking=True)
+    pin = hb.data.is_pinned()
+    n_off = (hb.off.size + 1) & ~1   # the interval table starts 16-byte aligned
+    host = np.zeros(n_off + ex.size, np.int64)
+    host[: hb.off.size] = hb.off.view(np.int64)
+    host[n_off:] = ex.view(np.int64)
+    small = torch.from_numpy(host)
+    if pin:
+        small = small.pin_memory()
+    small = small.to(dev, non_blocking=pin)
+    off, excl = small[: hb.off.size], small[n_off:]
     return DeviceBatch(data, off, excl, hb.n, hb.excl.size // 2)
 
 

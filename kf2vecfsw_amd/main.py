@@ -117,9 +117,22 @@ def get_frequencies(args) -> None:
     from concurrent.futures import ThreadPoolExecutor
 
     files_pool = ThreadPoolExecutor(max_workers=threads)
+    # KF_TRACE=1: per-batch stage timeline on stderr (host ms; device events ms
+    # from the first H2D's start event), for tools/e2e_bench.py
+    trace = os.environ.get("KF_TRACE") == "1"
+    import time
+    t_origin = time.perf_counter()
+    tr: list = []
+
+    def now_ms():
+        return round((time.perf_counter() - t_origin) * 1e3, 3)
 
     def pack(idx):
-        return pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool)
+        t0 = now_ms()
+        hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool)
+        if trace:
+            tr.append(("read", idx[0], t0, now_ms()))
+        return hb
 
     # Three-stage pipeline over batches:
     #   readers (2)   : read + record-index batches i+1, i+2 into pinned memory
@@ -135,23 +148,40 @@ def get_frequencies(args) -> None:
 
     def write(ev, host, hb, names):
         ev.synchronize()
+        t0 = now_ms()
         c = host.numpy().view(np.uint32)
         write_kf_files(args.output_dir, names, c, args.pseudocount, args.raw_cnt, args.p)
+        if trace:
+            tr.append(("write", names[0] if names else "", t0, now_ms()))
         del hb   # pinned input stays alive until the copies that read it are done
 
+    evs = []
     for bi, idx in enumerate(batches):
+        t_wait = now_ms()
         hb = reads.popleft().result()
+        if trace:
+            tr.append(("got", bi, t_wait, now_ms()))
         if bi + 2 < len(batches):
             reads.append(reader.submit(pack, batches[bi + 2]))
         with torch.cuda.stream(stream):
+            if trace:
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                e[0].record(stream)
+                evs.append((bi, now_ms(), e))
             db = to_device(hb, device)
+            if trace:
+                e[1].record(stream)
             counts, _ = counter.count(db, stream=stream.cuda_stream)
+            if trace:
+                e[2].record(stream)
             keep = [j for j, i in enumerate(idx) if last[samples_names[i]] == i]
             rows = counts if len(keep) == len(idx) else counts[torch.tensor(keep, device=device)]
             host = torch.empty(rows.shape, dtype=rows.dtype, pin_memory=True)
             host.copy_(rows, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)
+            if trace:
+                e[3].record(stream)
         for i in idx:
             if args.pseudocount:                       # main.py:332-333
                 print(">>> Adding pseudocounts. Sample: {}".format(files_names[i]))
@@ -163,6 +193,14 @@ def get_frequencies(args) -> None:
     reader.shutdown()
     writer.shutdown()
     files_pool.shutdown()
+    if trace and evs:
+        base_cpu = evs[0][1]
+        e00 = evs[0][2][0]
+        for bi, t_issue, e in evs:   # device times re-based on the first start event's host time
+            d = [round(base_cpu + e00.elapsed_time(x), 3) for x in e]
+            tr.append(("gpu", bi, t_issue, {"h2d": d[:2], "count": d[1:3], "d2h": d[2:4]}))
+        import json
+        print(json.dumps({"kf_trace": tr, "total_ms": now_ms()}), file=sys.stderr)
 
     print("\n==> Done processing {}".format(args.input_dir))
 

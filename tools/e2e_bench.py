@@ -84,6 +84,15 @@ def main():
             M.main(cli + extra)
             walls[tag].append(time.perf_counter() - t0)
     cli_s = min(walls["pipelined"])
+    # one traced pipelined run: per-batch stage timeline (KF_TRACE=1, stderr)
+    import contextlib
+    import io
+    buf = io.StringIO()
+    os.environ["KF_TRACE"] = "1"
+    with contextlib.redirect_stderr(buf):
+        M.main(cli)
+    del os.environ["KF_TRACE"]
+    trace = [json.loads(line)["kf_trace"] for line in buf.getvalue().splitlines() if line.startswith('{"kf_trace"')]
 
     # phase breakdown on the same files
     dev = torch.device("cuda:0")
@@ -111,7 +120,8 @@ def main():
            "phases_s": {k: round(v, 5) for k, v in ph.items()},
            "kernel_Gbases_s": round(bases / ph["kernel"] / 1e9, 1),
            "h2d_GBps": round(sum(sizes) / ph["h2d"] / 1e9, 1),
-           "parity_kf_byte_exact": f"{ok}/{len(files)}"}
+           "parity_kf_byte_exact": f"{ok}/{len(files)}",
+           "trace_pipelined": trace[0] if trace else None}
     print(json.dumps(res))
     shutil.rmtree(args.dir, ignore_errors=True)
     if ok != len(files):
