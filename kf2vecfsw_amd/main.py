@@ -63,12 +63,15 @@ def format_kf(name: str, counts: np.ndarray, pseudocount: bool = False, raw_cnt:
 
 
 def _pipeline_budget(paths: list[str], batch_gb) -> int:
-    """Bytes per batch: -batch_gb if given, else about a quarter of the input
-    (so reading, copying, counting and writing overlap) within [32 MiB, 4 GiB]."""
+    """Bytes per batch: -batch_gb if given, else about an eighth of the input
+    (so reading, copying, counting and writing overlap; measured best of 4-16
+    parts on 64 x 5 Mbp, tools/e2e_bench.py) within [16 MiB, 4 GiB].
+    KF_BATCH_PARTS overrides the part count."""
     if batch_gb:
         return int(float(batch_gb) * (1 << 30))
     total = sum(os.path.getsize(p) for p in paths)
-    return int(min(max(total // 4, 32 << 20), 4 << 30))
+    parts = int(os.environ.get("KF_BATCH_PARTS", "8"))
+    return int(min(max(total // parts, 16 << 20), 4 << 30))
 
 
 def _batches(paths: list[str], budget: int) -> list[list[int]]:
@@ -129,9 +132,10 @@ def get_frequencies(args) -> None:
 
     def pack(idx):
         t0 = now_ms()
-        hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool)
+        tm = {}
+        hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool, times=tm)
         if trace:
-            tr.append(("read", idx[0], t0, now_ms()))
+            tr.append(("read", idx[0], t0, now_ms(), tm))
         return hb
 
     # Three-stage pipeline over batches:
@@ -141,9 +145,10 @@ def get_frequencies(args) -> None:
     #   writer thread : wait for batch i's copy-back, format + write its .kf files
     # The prints stay in the reference's per-file order (main.py:332-341).
     stream = torch.cuda.Stream(device)
-    reader = ThreadPoolExecutor(max_workers=2)
+    depth = int(os.environ.get("KF_READ_AHEAD", "2"))   # batches being read ahead
+    reader = ThreadPoolExecutor(max_workers=depth)
     writer = ThreadPoolExecutor(max_workers=1)
-    reads = deque(reader.submit(pack, batches[i]) for i in range(min(2, len(batches))))
+    reads = deque(reader.submit(pack, batches[i]) for i in range(min(depth, len(batches))))
     writes = []
 
     def write(ev, host, hb, names):
@@ -161,8 +166,8 @@ def get_frequencies(args) -> None:
         hb = reads.popleft().result()
         if trace:
             tr.append(("got", bi, t_wait, now_ms()))
-        if bi + 2 < len(batches):
-            reads.append(reader.submit(pack, batches[bi + 2]))
+        if bi + depth < len(batches):
+            reads.append(reader.submit(pack, batches[bi + depth]))
         with torch.cuda.stream(stream):
             if trace:
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -171,23 +176,31 @@ def get_frequencies(args) -> None:
             db = to_device(hb, device)
             if trace:
                 e[1].record(stream)
+                th = [now_ms()]
             counts, _ = counter.count(db, stream=stream.cuda_stream)
             if trace:
                 e[2].record(stream)
+                th.append(now_ms())
             keep = [j for j, i in enumerate(idx) if last[samples_names[i]] == i]
             rows = counts if len(keep) == len(idx) else counts[torch.tensor(keep, device=device)]
             host = torch.empty(rows.shape, dtype=rows.dtype, pin_memory=True)
+            if trace:
+                th.append(now_ms())
             host.copy_(rows, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)
             if trace:
                 e[3].record(stream)
+                th.append(now_ms())
         for i in idx:
             if args.pseudocount:                       # main.py:332-333
                 print(">>> Adding pseudocounts. Sample: {}".format(files_names[i]))
             if not args.raw_cnt:                       # main.py:340-341
                 print(">>> Normalizing. Sample: {}".format(files_names[i]))
         writes.append(writer.submit(write, ev, host, hb, [samples_names[idx[j]] for j in keep]))
+        if trace:
+            th.append(now_ms())
+            tr.append(("issue", bi, th))   # after: to_device, count, pinned alloc, D2H, prints+submit
     for w in writes:
         w.result()
     reader.shutdown()
