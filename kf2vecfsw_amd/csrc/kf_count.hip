@@ -37,16 +37,19 @@ namespace kf {
 //   variant 0: 512 threads (8 waves), 2 workgroups/CU at k=7
 //   variant 1: 1024 threads (16 waves), 8 waves/SIMD register budget
 //   variant 2: as 1 with a 6-deep chunk prefetch ring (5 chunks in flight)
-#ifdef KF_ABLATION
-constexpr int kNumVariants = 5;
-#else
-constexpr int kNumVariants = 3;
-#endif
+//   variants 5..7: k = 7 pair counting (pair_kernel below), one 1024-thread
+//             workgroup per CU (160 KiB of LDS), 4 waves/SIMD, prefetch ring 6 / 4 / 8;
+//             for every other k they run as variant 1
+constexpr int kNumVariants = 8;
 constexpr int kDefaultVariant = 1;
+constexpr int kFirstPairVariant = 5;
 template <int V> struct Shape;
 template <> struct Shape<0> { static constexpr int block = 512, wpe = 0, abl = 0, ring = 4; };
 template <> struct Shape<1> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 4; };
 template <> struct Shape<2> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 6; };
+template <> struct Shape<5> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 6; };
+template <> struct Shape<6> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 4; };
+template <> struct Shape<7> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 8; };
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
 template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 1, ring = 4; };   // no LDS adds
@@ -181,6 +184,296 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
     return win.next;
 }
 
+// ---------------------------------------------------------------- k = 7 pair counting
+// Two consecutive 7-mer windows are one 8-mer: its first seven bases are the
+// older window, its last seven the newer one.  The fast path counts the windows
+// of a chunk in pairs, one LDS atomic per pair instead of one per window, into
+// P = 4^8 u16 counters (128 KiB: 8-mer x in half x & 1 of word x >> 1).  Windows
+// left unpaired (an odd chunk total, and every window of an irregular chunk) go
+// to S, 8192 u16 counters (16 KiB) indexed by the 7-mer folded to the orientation
+// whose middle base is A or C (s_fold): one slot per canonical 7-mer.  At flush a
+// canonical column with forward representative y gets
+//   F(y) + F(rc y) + S[fold y],  F(y) = sum_a P[4y + a] + sum_a P[a 4^7 + y]
+// (y as the older window of a pair, then as the newer one).
+// u16 halves: every add returns the old word; a half that has reached 0x4000 is
+// moved to the genome's count row (pair_drain).  At most two chunks of adds per
+// wave (16 waves x 2 x 1024) can land on a half between its crossing and the
+// first drain, so it stays below 0x4000 + 0x8000: the counts are exact.
+constexpr uint32_t kPairSBase = 1u << 17;                    // byte offset of S
+constexpr uint32_t kPairCtl = kPairSBase + (1u << 14);       // two chunk counters (pair_kernel)
+constexpr uint32_t kPairLdsBytes = kPairCtl + 16;
+constexpr uint32_t kU16Hot = 0xC000C000u;                    // a half >= 0x4000
+#ifndef KF_PAIR_ABL
+#define KF_PAIR_ABL 0
+#endif
+
+__device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
+    return __hip_atomic_fetch_add((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// 7-mer (kf code, A0 C1 T2 G3, complement = ^2) -> S slot: the orientation whose
+// middle base (bits 6-7) has bit 7 clear, with that bit dropped.
+__device__ __forceinline__ uint32_t s_fold(uint32_t y, uint32_t rc) {
+    const uint32_t z = (y & 0x80u) ? rc : y;
+    return ((z >> 8) << 7) | (z & 0x7Fu);
+}
+__device__ __forceinline__ uint32_t s_unfold(uint32_t i) { return ((i >> 7) << 8) | (i & 0x7Fu); }
+__device__ __forceinline__ uint32_t s_addr(uint32_t i) { return kPairSBase + ((i >> 1) << 2); }
+__device__ __forceinline__ uint32_t half_one(uint32_t i) { return 1u << ((i & 1u) << 4); }
+
+// Rare path: move 0x4000 out of each half of the LDS word at byte address a that
+// has reached it, into the count row (compare-and-swap: each move happens once).
+__device__ __noinline__ void pair_drain(uint32_t a, const uint32_t* __restrict__ code2col, uint32_t* gcounts) {
+    lds_u32* p = (lds_u32*)(uintptr_t)a;
+    uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (cur & kU16Hot) {
+        const uint32_t sub = ((cur & 0xC0000000u) ? 0x40000000u : 0u) | ((cur & 0xC000u) ? 0x4000u : 0u);
+        uint32_t seen = cur;
+        if (__hip_atomic_compare_exchange_strong(p, &seen, cur - sub, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            const bool single = a >= kPairSBase;
+            const uint32_t w = (single ? a - kPairSBase : a) >> 2;
+            for (uint32_t h = 0; h < 2; ++h) {
+                if (!((sub >> (16 * h)) & 0x4000u)) continue;
+                const uint32_t bin = 2 * w + h;   // 8-mer (P) or S slot
+                if (single) {
+                    atomicAdd(gcounts + code2col[s_unfold(bin)], 0x4000u);
+                } else {
+                    atomicAdd(gcounts + code2col[bin >> 2], 0x4000u);
+                    atomicAdd(gcounts + code2col[bin & 0x3FFFu], 0x4000u);
+                }
+            }
+            cur -= sub;
+        } else {
+            cur = seen;
+        }
+    }
+}
+
+// Exclusive count of set bits of m below this lane.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// 1 << byte b of h (the byte is 0 or 16): one SDWA shift.
+template <int B>
+__device__ __forceinline__ uint32_t shl1_byte(uint32_t h, uint32_t one) {
+    uint32_t r;
+    if constexpr (B == 0)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+            : "=v"(r) : "v"(h), "v"(one));
+    else if constexpr (B == 1)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+            : "=v"(r) : "v"(h), "v"(one));
+    else if constexpr (B == 2)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+            : "=v"(r) : "v"(h), "v"(one));
+    else
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+            : "=v"(r) : "v"(h), "v"(one));
+    return r;
+}
+
+// A pair-kernel chunk is self-contained: lane 0 loads the 16 bytes before the
+// chunk's own 1008 (63 lanes x 16 B), which give lane 1 its k-1 bases of context,
+// and counts nothing itself.  So chunks need no carry from their predecessor and
+// the waves of a workgroup can take them in any order (pair_kernel hands them out
+// from an LDS counter).  Chunk c of a piece owns [c0 + 1008 c, c0 + 1008 (c+1)).
+constexpr uint32_t kOwn = kChunk - 16;
+
+// Chunk bookkeeping is 32-bit relative to c0 (a piece is far below 4 GiB) so it
+// stays on the SALU: gfx9 has no 64-bit ordered scalar compare.
+struct PPiece {
+    uint64_t glo, plo, phi, c0;
+    const uint8_t* pb16;   // bytes + c0 - 16: lane 0's block of chunk 0
+    uint32_t nch;          // chunks
+    uint32_t end_r;        // align16(ghi) - c0: readable bytes
+    uint32_t fast_lo;      // chunks whose own bytes start at >= fast_lo ...
+    uint32_t fast_hi;      // ... and end at <= fast_hi can take the fast path
+    uint32_t skip0;        // chunk 0's lane-0 block would start before the genome
+};
+__device__ __forceinline__ PPiece make_piece(const uint8_t* bytes, uint64_t glo, uint64_t ghi, uint64_t plo,
+                                             uint64_t phi) {
+    PPiece P;
+    P.glo = glo, P.plo = plo, P.phi = phi;
+    P.c0 = plo & ~(uint64_t)15;
+    P.pb16 = bytes + P.c0 - 16;
+    const uint64_t gal = glo & ~(uint64_t)15;
+    P.skip0 = P.c0 < gal + 16 ? 16u : 0u;
+    P.end_r = (uint32_t)(((ghi + 15) & ~(uint64_t)15) - P.c0);
+    P.nch = phi > plo ? (uint32_t)((phi - P.c0 + kOwn - 1) / kOwn) : 0u;
+    P.fast_lo = (uint32_t)(max(glo + 16, plo) - P.c0);
+    P.fast_hi = (uint32_t)(phi - P.c0);
+    return P;
+}
+// Lane block of chunk c (zeros for c >= nch, without touching memory).  Lane 0
+// of a chunk whose context would start before the genome's aligned start reads
+// zeros (its offset wraps past num_records), never bytes before the buffer.
+__device__ __forceinline__ uint4 pload(const PPiece& P, uint32_t c, int lane) {
+    const uint32_t adj = c == 0 ? P.skip0 : 0u;
+    const uint32_t b16 = kOwn * c + adj;   // descriptor base - (c0 - 16)
+    const uint32_t avail = P.end_r + 16u > b16 ? P.end_r + 16u - b16 : 0u;
+    // (readfirstlane: keeps the descriptor in SGPRs; the compiler turns the clamp
+    // above into a VALU saturating subtract and would waterfall the load)
+    const uint32_t rec = __builtin_amdgcn_readfirstlane(c < P.nch ? min(avail, (uint32_t)kChunk) : 0u);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(P.pb16 + b16), (short)0, (int)rec, 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(16 * lane) - adj, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// Excluded-interval cursor of a wave (its chunks come in increasing order);
+// s_r / e_r: the current interval relative to the piece's c0 - 16, clamped.
+struct IvCursor {
+    uint64_t iv;
+    uint32_t s_r, e_r;
+    __device__ __forceinline__ void init(const CountArgs& A, uint64_t pos, int lane) {
+        iv = wave_upper_bound(A.n_excl, pos, lane, [&](uint64_t i) { return A.excl[2 * i + 1]; });
+    }
+    // (signed: c0 - 16 is negative for a piece in the buffer's first 16 bytes)
+    __device__ __forceinline__ static uint32_t rel(uint64_t x, int64_t o) {
+        const int64_t d = (int64_t)x - o;
+        return d <= 0 ? 0u : (d >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)d);
+    }
+    __device__ __forceinline__ void load(const CountArgs& A, const PPiece& P) {
+        s_r = e_r = 0xFFFFFFFFu;
+        if (iv < A.n_excl) {
+            s_r = rel(uload64(A.excl + 2 * iv), (int64_t)P.c0 - 16);
+            e_r = rel(uload64(A.excl + 2 * iv + 1), (int64_t)P.c0 - 16);
+        }
+    }
+    // true if an interval overlaps [a, b) (relative to c0 - 16); first moves past
+    // intervals ending <= a
+    __device__ __forceinline__ bool hits(const CountArgs& A, const PPiece& P, uint32_t a, uint32_t b) {
+        if (e_r <= a) {   // rare
+            const int64_t aa = (int64_t)P.c0 - 16 + (int64_t)a;
+            do { ++iv; } while (iv < A.n_excl && (int64_t)uload64(A.excl + 2 * iv + 1) <= aa);
+            load(A, P);
+        }
+        return s_r < b;
+    }
+};
+
+template <bool MASKED>
+__device__ __forceinline__ void count_chunk_ind(const uint4 d, const CountArgs& A, const PPiece& P, uint32_t c,
+                                                int lane, uint64_t iv0, uint32_t* gcounts, uint32_t& lane_total) {
+    constexpr int K = 7;
+    const uint64_t own = P.c0 + (uint64_t)kOwn * c;
+    if constexpr (!MASKED) {
+        uint32_t Cf, NNL, bad;
+        classify16_fast(d, Cf, NNL, bad);
+        const uint32_t nef = (uint32_t)__builtin_popcount(NNL);
+        const bool self_ok = bad == 0 && nef >= 15u;
+        if (__builtin_amdgcn_ballot_w64(!self_ok) == 0) {
+            // every block is bases with at most one newline: lane 0's 15-16 bases are
+            // lane 1's context; drop the newline entry, context from lane L-1
+            const uint32_t r = (uint32_t)__builtin_ctz((NNL ^ 0xFFFFu) | 0x10000u);
+            const uint32_t lo1 = (1u << r) - 1u, lo2 = lo1 | (lo1 << r);
+            const uint32_t C = bfi(lo2, Cf, Cf >> 2);
+            const uint32_t pC = wave_shr1(0u, C);
+            // The windows of lanes 1..63 in stream order are paired (0,1), (2,3), ...;
+            // a lane owns the pairs whose newer window is its own.  p = parity of the
+            // windows in lanes 1..L-1 (lanes with 15 entries are the odd ones); pairs
+            // then end at entries q, q+2, ... (entry 0 = newest).
+            const uint32_t p = lanes_below(__builtin_amdgcn_ballot_w64(nef == 15u) & ~1ull) & 1u;
+            const uint32_t q = (nef + p) & 1u;
+            const uint64_t W = (((uint64_t)pC << (2u * nef)) | (uint64_t)C) >> (2u * q);
+            const uint32_t lo = (uint32_t)W, hi = (uint32_t)(W >> 32);
+            // pair j = 8-mer at bits [4j, 4j+16) of W: word (x >> 1) at byte address
+            // bits [4j+1, 4j+16) << 2, half = bit 4j (as 16 x that bit, one per byte)
+            const uint32_t H0 = (lo << 4) & 0x10101010u, H1 = lo & 0x10101010u;
+            const uint32_t one = 1u;
+            const bool has7 = !(nef == 15u && p == 0u);   // pair 7 would end at entry 15
+            auto paddr = [&](int j) -> uint32_t {
+                return (j == 0 ? (lo << 1) : __builtin_amdgcn_alignbit(hi, lo, 4 * j - 1)) & 0x1FFFCu;
+            };
+            uint32_t o = 0;
+            const bool single = lane == kWave - 1 && q;   // odd total: the newest window is unpaired
+            if (lane != 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    uint32_t dl;
+                    switch (j) {
+                    case 0: dl = shl1_byte<0>(H0, one); break;
+                    case 1: dl = shl1_byte<0>(H1, one); break;
+                    case 2: dl = shl1_byte<1>(H0, one); break;
+                    case 3: dl = shl1_byte<1>(H1, one); break;
+                    case 4: dl = shl1_byte<2>(H0, one); break;
+                    case 5: dl = shl1_byte<2>(H1, one); break;
+                    case 6: dl = shl1_byte<3>(H0, one); break;
+                    default: dl = has7 ? shl1_byte<3>(H1, one) : 0u; break;
+                    }
+#if KF_PAIR_ABL == 1   // profiling only: no returns, no overflow check (wrong on low complexity)
+                    lds_add(paddr(j), dl);
+#elif KF_PAIR_ABL == 2   // profiling only: no pair adds at all
+                    lane_total += paddr(j) ^ dl;
+#else
+                    o |= lds_add_rtn(paddr(j), dl);
+#endif
+                }
+                lane_total += nef;
+                if (single) {
+                    const uint32_t y = C & 0x3FFFu;
+                    const uint32_t i = s_fold(y, kf_revcomp<K>(y));
+                    o |= lds_add_rtn(s_addr(i), half_one(i));
+                }
+            }
+            if (__builtin_amdgcn_ballot_w64((o & kU16Hot) != 0) != 0 && (o & kU16Hot)) {
+                // rare: some word this lane added to is hot; re-check all of them
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pair_drain(paddr(j), A.code2col, gcounts);
+                if (single) {
+                    const uint32_t y = C & 0x3FFFu;
+                    pair_drain(s_addr(s_fold(y, kf_revcomp<K>(y))), A.code2col, gcounts);
+                }
+            }
+            return;
+        }
+    }
+    // irregular chunk: every counted window as a single 7-mer into S
+    const uint64_t B = own - 16;   // lane 0's block (may lie before the genome: invalid)
+    const ChunkMask m{P.glo, max(own, P.plo), min(own + kOwn, P.phi)};
+    uint32_t C, V, EN, ne, own_t;
+    front_end<K, true>(d, A, B, lane, m, iv0, C, V, EN, ne, own_t);
+    // lane 1 needs exact context: lane 0's block if its tail is complete, else walk back
+    uint32_t carry = tail_pack(0, 0, 0);
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)own_t, 0);
+    if (!tail_complete<K>(t0)) {   // rare: fewer than k-1 bases and no reset in 16 bytes
+        for (int64_t p = (int64_t)B; p > (int64_t)P.glo && !tail_complete<K>(carry);) {
+            p -= kChunk;
+            carry = tail_combine<K>(chunk_tail<K>(A.bytes, A.excl, A.n_excl, p, P.glo, lane), carry);
+        }
+    }
+    const Windows win = windows<K, true>(C, V, EN, ne, carry, lane);
+    const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
+    const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
+                            __builtin_amdgcn_alignbit(whi, wlo, 24)};
+    auto fwd = [&](int r) -> uint32_t {
+        const int fo = (2 * r) & ~7;
+        return __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, 2 * K);
+    };
+    // reverse complement of the 64-bit window: revcomp of window r = bits [2(15-r), +2K) of RP
+    const uint32_t rhi = revpairs(wlo) ^ 0xAAAAAAAAu, rlo = revpairs(whi) ^ 0xAAAAAAAAu;
+    constexpr int RS = 2 * (17 - K);
+    const uint32_t rplo = __builtin_amdgcn_alignbit(rhi, rlo, RS), rphi = rhi >> RS;
+    const uint32_t rv[4] = {rplo, __builtin_amdgcn_alignbit(rphi, rplo, 8), __builtin_amdgcn_alignbit(rphi, rplo, 16),
+                            __builtin_amdgcn_alignbit(rphi, rplo, 24)};
+    auto rcw = [&](int r) -> uint32_t {
+        const int rr = 2 * (15 - r), ro = rr & ~7;
+        return __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, 2 * K);
+    };
+    uint32_t o = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t i = s_fold(fwd(r), rcw(r));
+        o |= lds_add_rtn(s_addr(i), ((R >> r) & 1u) * half_one(i));
+    }
+    if (__builtin_amdgcn_ballot_w64((o & kU16Hot) != 0) != 0 && (o & kU16Hot)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pair_drain(s_addr(s_fold(fwd(r), rcw(r))), A.code2col, gcounts);
+    }
+    lane_total += (uint32_t)__builtin_popcount(R);
+}
+
 // Process the wave range [lo, hi) of genome [glo, ghi).
 template <int K, bool GLOBAL, int ABL, int RING>
 __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
@@ -275,6 +568,8 @@ __global__ void __launch_bounds__(Shape<V>::block)
     const uint64_t span_hi = (b + 1 == G) ? base + total
                                           : base + ((total / G * (b + 1) + (total % G) * (b + 1) / G) & ~(uint64_t)15);
     if (span_lo >= span_hi) return;
+    const uint64_t tk0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;        // shader clock
+    const uint64_t rt0 = A.prof ? __builtin_amdgcn_s_memrealtime() : 0;    // 100 MHz
     // first genome whose end is beyond span_lo
     int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, span_lo, lane,
                                           [&](uint64_t i) { return A.goff[i + 1]; });
@@ -346,6 +641,209 @@ __global__ void __launch_bounds__(Shape<V>::block)
             for (int w = 0; w < kWaves; ++w) t += red[w];
             if (t) atomicAdd(A.totals + g, t);
         }
+    }
+    if (A.prof && tid == 0) {
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(A.prof + 40, (unsigned long long)(__builtin_amdgcn_s_memtime() - tk0));
+        atomicAdd(A.prof + 41, (unsigned long long)(rt1 - rt0));
+        atomicMin(A.prof + 42, (unsigned long long)rt0);
+        atomicMax(A.prof + 43, (unsigned long long)rt1);
+        atomicMax(A.prof + 44, (unsigned long long)(rt1 - rt0));
+        atomicMax(A.prof + 45, (unsigned long long)rt0);
+    }
+}
+
+// k = 7 pair counting kernel: same spans as count_kernel, one workgroup per CU
+// holding P and S (144 KiB), so nothing else on the CU hides a stall; the kernel
+// keeps the byte stream busy instead:
+// * the 16 waves take self-contained chunks (count_chunk_ind) of the current
+//   genome piece from an LDS counter, RING chunks ahead, so they finish a piece
+//   together although a SIMD issues oldest-first (its 4th wave gets about half
+//   the issue slots of its 1st);
+// * at the end of a piece each wave takes and loads the next piece's first RING
+//   chunks before the flush, so the flush runs under those loads;
+// * flush: every 8-mer counter is read once, with lane-consecutive addresses,
+//   into per-7-mer sums F (y as the older window + y as the newer window), which
+//   go back to LDS; a column then needs F[rep] + F[rc rep] + S.
+__device__ __forceinline__ uint32_t u16sum2(uint32_t w) { return (w & 0xFFFFu) + (w >> 16); }
+
+// Next genome piece of this workgroup at or after genome g (g = n: none).
+__device__ __forceinline__ int32_t pair_next_piece(const CountArgs& A, int32_t g, uint64_t span_lo, uint64_t span_hi,
+                                                   PPiece& P) {
+    for (; g < A.n_genomes; ++g) {
+        const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
+        if (glo >= span_hi) break;
+        const uint64_t plo = max(glo, span_lo), phi = min(ghi, span_hi);
+        if (phi > plo) {
+            P = make_piece(A.bytes, glo, ghi, plo, phi);
+            return g;
+        }
+    }
+    P = make_piece(A.bytes, 0, 0, 0, 0);
+    return A.n_genomes;
+}
+
+__device__ __forceinline__ uint32_t pair_grab(uint32_t ctr, int lane) {
+    uint32_t t = 0;
+    if (lane == 0) t = lds_add_rtn(ctr, 1u);
+    return t;
+}
+
+template <int V>
+__global__ void __launch_bounds__(Shape<V>::block) __attribute__((amdgpu_waves_per_eu(Shape<V>::wpe, Shape<V>::wpe)))
+    pair_kernel(CountArgs A) {
+    constexpr int K = 7;
+    constexpr int kBlock = Shape<V>::block;
+    constexpr int RING = Shape<V>::ring;
+    static_assert(kBlock == 1024, "pair_kernel flush assumes 1024 threads");
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint4* h4 = (uint4*)hist;
+    for (uint32_t i = tid; i < kPairLdsBytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    if ((uint32_t)(uintptr_t)(lds_u32*)hist != 0u) __builtin_trap();   // addresses assume LDS base 0
+
+    const uint64_t base = A.goff[0];
+    const uint64_t total = A.goff[A.n_genomes] - base;
+    const uint64_t G = gridDim.x, b = blockIdx.x;
+    const uint64_t span_lo = base + ((total / G * b + (total % G) * b / G) & ~(uint64_t)15);
+    const uint64_t span_hi = (b + 1 == G) ? base + total
+                                          : base + ((total / G * (b + 1) + (total % G) * (b + 1) / G) & ~(uint64_t)15);
+    if (span_lo >= span_hi) return;
+    const uint64_t tk0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;        // shader clock
+    const uint64_t rt0 = A.prof ? __builtin_amdgcn_s_memrealtime() : 0;    // 100 MHz
+    int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, span_lo, lane,
+                                          [&](uint64_t i) { return A.goff[i + 1]; });
+    PPiece P;
+    g = pair_next_piece(A, g, span_lo, span_hi, P);
+    if (g >= A.n_genomes) return;
+    IvCursor cur;
+    cur.init(A, P.c0 >= 16 ? P.c0 - 16 : 0, lane);
+    cur.load(A, P);
+    uint32_t par = 0;   // counter of the current piece: kPairCtl + 4 par
+    uint32_t idx[RING];
+    uint4 buf[RING];
+#pragma unroll
+    for (int j = 0; j < RING; ++j) {
+        idx[j] = __builtin_amdgcn_readfirstlane(pair_grab(kPairCtl, lane));
+        buf[j] = pload(P, idx[j], lane);
+    }
+    for (;;) {
+        const uint64_t t0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+        const uint32_t ctr = kPairCtl + 4 * par;
+        uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
+        uint32_t lt = 0, nproc = 0;
+        for (;;) {
+#pragma unroll
+            for (int j = 0; j < RING; ++j) {
+                const uint32_t tok = pair_grab(ctr, lane);   // refill of this slot, used below
+                const uint32_t c = idx[j];
+                if (c < P.nch) {
+                    const uint32_t own_r = kOwn * c;   // own bytes start at c0 + own_r
+                    const bool msk = own_r < P.fast_lo || own_r + kOwn > P.fast_hi ||
+                                     cur.hits(A, P, own_r, own_r + kChunk);
+#if KF_PAIR_ABL == 3   // profiling only: stream the bytes, no counting
+                    lt += buf[j].x ^ buf[j].y ^ buf[j].z ^ buf[j].w;
+                    (void)msk;
+#else
+                    if (msk)
+                        count_chunk_ind<true>(buf[j], A, P, c, lane, cur.iv, gc, lt);
+                    else
+                        count_chunk_ind<false>(buf[j], A, P, c, lane, cur.iv, gc, lt);
+#endif
+                    ++nproc;
+                }
+                idx[j] = __builtin_amdgcn_readfirstlane(tok);
+                buf[j] = pload(P, idx[j], lane);
+            }
+            uint32_t mn = idx[0];
+#pragma unroll
+            for (int j = 1; j < RING; ++j) mn = min(mn, idx[j]);
+            if (mn >= P.nch) break;
+        }
+        const unsigned long long s = wave_sum(lt);
+        if (lane == 0 && s) atomicAdd(A.totals + g, s);
+        const uint64_t t1 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+        if (A.prof && lane == 0) {
+            atomicAdd(A.prof + 1, (unsigned long long)(t1 - t0));
+            atomicAdd(A.prof + 2, 1ull);
+            atomicAdd(A.prof + 8 + wave, (unsigned long long)(t1 - t0));
+            atomicAdd(A.prof + 24 + wave, (unsigned long long)nproc);
+        }
+        __syncthreads();   // (A) every add of this piece is done
+        const uint64_t t_f1 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+        const int32_t gcur = g;
+        // the columns' forward representatives: loaded before the next piece's byte
+        // stream, so their wait does not queue behind it (loads return in order)
+        uint32_t rep[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) rep[c] = A.col2rep[tid + c * kBlock];
+        PPiece Pn;
+        g = pair_next_piece(A, g + 1, span_lo, span_hi, Pn);
+        // flush (1): per forward 7-mer y, F(y) = sum_a P[4y + a] + sum_a P[a 4^7 + y];
+        // thread t owns y = 2048 i + 2t + {0, 1}, i = 0..7 (lane-consecutive reads)
+        uint32_t F[16];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint4 w = h4[i * 1024 + tid];   // words 2y .. 2y+3 of y = 2048 i + 2 tid
+            F[2 * i] = u16sum2(w.x) + u16sum2(w.y);
+            F[2 * i + 1] = u16sum2(w.z) + u16sum2(w.w);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const uint32_t v = hist[a * 8192 + i * 1024 + tid];   // halves a 4^7 + y, a 4^7 + y + 1
+                F[2 * i] += v & 0xFFFFu;
+                F[2 * i + 1] += v >> 16;
+            }
+        }
+        __syncthreads();   // (B) P read
+#pragma unroll
+        for (int i = 0; i < 8; ++i) *(uint2*)(hist + i * 2048 + 2 * tid) = make_uint2(F[2 * i], F[2 * i + 1]);
+        // next piece: its first chunks taken and in flight under the rest of the flush
+        // (not earlier: the ring and F together would not fit in 128 VGPRs)
+        const uint32_t ctr_next = kPairCtl + 4 * (par ^ 1u);
+#pragma unroll
+        for (int j = 0; j < RING; ++j) {
+            idx[j] = __builtin_amdgcn_readfirstlane(pair_grab(ctr_next, lane));
+            buf[j] = pload(Pn, idx[j], lane);
+        }
+        __syncthreads();   // (C) F in LDS words [0, 16384)
+        const uint16_t* S = (const uint16_t*)((const uint8_t*)hist + kPairSBase);
+        uint32_t* gcf = A.counts + (uint64_t)gcur * A.nbins;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t y = rep[c], rc = kf_revcomp<K>(y);
+            const uint32_t v = hist[y] + hist[rc] + S[s_fold(y, rc)];
+            if (v) __hip_atomic_fetch_add(gcf + tid + c * kBlock, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();   // (D) columns read
+        for (uint32_t i = tid; i < kPairCtl / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (tid == 0) hist[kPairCtl / 4 + par] = 0;   // this piece's counter, for the piece after next
+        const uint64_t t_f2 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+        __syncthreads();   // (E) P, S and the counter zero
+        if (A.prof && tid == 0) {
+            const uint64_t t_f3 = __builtin_amdgcn_s_memtime();
+            atomicAdd(A.prof + 3, (unsigned long long)(t_f1 - t1));
+            atomicAdd(A.prof + 4, 1ull);
+            atomicAdd(A.prof + 5, (unsigned long long)(t_f2 - t_f1));
+            atomicAdd(A.prof + 6, (unsigned long long)(t_f3 - t_f2));
+        }
+        if (g >= A.n_genomes) {
+            if (A.prof && tid == 0) {
+                const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+                atomicAdd(A.prof + 40, (unsigned long long)(__builtin_amdgcn_s_memtime() - tk0));
+                atomicAdd(A.prof + 41, (unsigned long long)(rt1 - rt0));
+                atomicMin(A.prof + 42, (unsigned long long)rt0);
+                atomicMax(A.prof + 43, (unsigned long long)rt1);
+                atomicMax(A.prof + 44, (unsigned long long)(rt1 - rt0));
+                atomicMax(A.prof + 45, (unsigned long long)rt0);
+            }
+            break;
+        }
+        P = Pn;
+        cur.load(A, P);   // re-base the interval cursor on the new piece
+        par ^= 1u;
     }
 }
 
@@ -483,7 +981,17 @@ void* count_kernel_v(int k) {
     }
 }
 
+// Variants >= kFirstPairVariant are the pair kernel at k = 7 and variant 1 elsewhere.
+bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant; }
+int effective_variant(int k, int v) { return (v >= kFirstPairVariant && !is_pair(k, v)) ? 1 : v; }
+
 void* count_kernel_for(int k, int v) {
+    if (is_pair(k, v)) {
+        if (v == 6) return (void*)&pair_kernel<6>;
+        if (v == 7) return (void*)&pair_kernel<7>;
+        return (void*)&pair_kernel<5>;
+    }
+    v = effective_variant(k, v);
 #ifdef KF_ABLATION
     if (v == 3) return count_kernel_v<3>(k);
     if (v == 4) return count_kernel_v<4>(k);
@@ -511,8 +1019,10 @@ int current_variant() {
     return (v >= 0 && v < kNumVariants) ? v : kDefaultVariant;
 }
 
-// histogram (4^k u32) + one u64 reduction slot per wave (16 waves max)
-int lds_bytes_for(int k) {
+// histogram (4^k u32) + one u64 reduction slot per wave (16 waves max); pair
+// kernel: P + S, nothing else
+int lds_bytes_for(int k, int v) {
+    if (is_pair(k, v)) return (int)kPairLdsBytes;
     if (k <= kLdsMaxK) return (int)(sizeof(uint32_t) << (2 * k)) + 16 * 8;
     if (k <= kMultiMaxK) return (int)(sizeof(uint32_t) << kMultiBits) + 16 * 8;
     return 0;
@@ -529,7 +1039,7 @@ int launch_info(int k, int* grid, int* block, int* lds, int* variant) {
     if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
     if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
     const int v = current_variant();
-    const int l = lds_bytes_for(k);
+    const int l = lds_bytes_for(k, v);
     std::lock_guard<std::mutex> lk(g_cache_mu);
     int& gr = g_cache.grid[k][v][dev];
     if (!gr) {
@@ -593,7 +1103,8 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.prof = nullptr;
     const char* pe = getenv("KF_COUNT_PROFILE");   // debugging aid: synchronous, prints to stderr
     if (pe && *pe == '1' && !bucket) {
-        if (hipMalloc((void**)&A.prof, 40 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 40 * 8, s) != hipSuccess)
+        if (hipMalloc((void**)&A.prof, 48 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 48 * 8, s) != hipSuccess ||
+            hipMemsetAsync(A.prof + 42, 0xFF, 8, s) != hipSuccess)
             return kf_fail(KF_EHIP, "profile buffer");
     }
     if (bucket) return bucket_launch(A, k, flags, s);
@@ -601,17 +1112,31 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     int rc = launch_info(k, &grid, &block, &lds, &variant);
     if (rc) return rc;
     void* args[] = {&A};
+    hipEvent_t pe0 = nullptr, pe1 = nullptr;
+    if (A.prof && (hipEventCreate(&pe0) != hipSuccess || hipEventCreate(&pe1) != hipSuccess ||
+                   hipEventRecord(pe0, s) != hipSuccess))
+        return kf_fail(KF_EHIP, "profile events");
     if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (A.prof) {
-        unsigned long long h[40];
-        if (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(h, A.prof, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
+        unsigned long long h[48];
+        float ms = 0.f;
+        if (hipEventRecord(pe1, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess ||
+            hipEventElapsedTime(&ms, pe0, pe1) != hipSuccess ||
+            hipMemcpy(h, A.prof, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
             return kf_fail(KF_EHIP, "profile readback");
+        (void)hipEventDestroy(pe0);
+        (void)hipEventDestroy(pe1);
+        fprintf(stderr, "  kernel %.3f ms (events); workgroup lifetime mean %.3f max %.3f ms; first start to "
+                "last end %.3f ms, last start %.3f ms after the first\n", ms, (double)h[41] / (double)grid * 1e-5,
+                (double)h[44] * 1e-5, (double)(h[43] - h[42]) * 1e-5, (double)(h[45] - h[42]) * 1e-5);
         (void)hipFree(A.prof);
         const double nf = h[4] ? (double)h[4] : 1.0, nr = h[2] ? (double)h[2] : 1.0;
         fprintf(stderr, "[count_kernel k=%d] wave ranges %llu: setup %.3g cyc/range, loop %.3g cyc/range; "
                 "flushes %llu (wave 0): barrier-in %.3g, flush %.3g, barrier-out %.3g cyc\n", k, h[2],
                 (double)h[0] / nr, (double)h[1] / nr, h[4], (double)h[3] / nf, (double)h[5] / nf, (double)h[6] / nf);
+        if (h[41])
+            fprintf(stderr, "  shader clock %.3f GHz over the workgroups' lifetimes\n", (double)h[40] / (double)h[41] * 0.1);
         for (int w = 0; w < 16; ++w)
             if (h[24 + w])
                 fprintf(stderr, "  wave %2d: %.0f cyc/chunk over %llu chunks\n", w, (double)h[8 + w] / h[24 + w],
@@ -628,7 +1153,9 @@ extern "C" int kf_stream_probe(const uint8_t* d_bytes, uint64_t n, uint32_t* d_o
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return kf_fail(KF_EHIP, "device query failed");
-    hipLaunchKernelGGL(stream_probe_kernel, dim3(2 * (cus > 0 ? cus : 1)), dim3(1024), 0, (hipStream_t)stream,
+    const char* wpc = getenv("KF_PROBE_WGS_PER_CU");   // measurement knob: 1024-thread workgroups per CU
+    const int per_cu = (wpc && atoi(wpc) >= 1 && atoi(wpc) <= 2) ? atoi(wpc) : 2;
+    hipLaunchKernelGGL(stream_probe_kernel, dim3(per_cu * (cus > 0 ? cus : 1)), dim3(1024), 0, (hipStream_t)stream,
                        d_bytes, n, d_out);
     if (hipGetLastError() != hipSuccess) return kf_fail(KF_EHIP, "stream probe launch failed");
     return KF_OK;

@@ -296,18 +296,24 @@ __device__ __forceinline__ uint64_t wave_upper_bound(uint64_t n, uint64_t x, int
     return a + (uint64_t)__builtin_popcountll(__ballot(i < b && key(i) <= x));
 }
 
-// Inclusive tail of the 1 KiB chunk starting at p (warm-up only; p may lie
-// before glo or even before the buffer: those bytes read as invalid).
+// Lane block of the 1 KiB chunk at p for chunk_tail_data (bytes before the
+// genome's aligned start read as zero, so p may lie before the buffer).
+__device__ __forceinline__ uint4 chunk_tail_load(const uint8_t* bytes, int64_t p, uint64_t glo, int lane) {
+    const int64_t b0 = p + 16 * lane;
+    uint4 d = make_uint4(0u, 0u, 0u, 0u);
+    if (b0 >= (int64_t)(glo & ~(uint64_t)15)) d = *(const uint4*)(bytes + b0);
+    return d;
+}
+
+// Inclusive tail of the 1 KiB chunk starting at p whose lane block d is already
+// loaded (warm-up only; bytes before glo are invalid).
 template <int K>
-__device__ __noinline__ uint32_t chunk_tail(const uint8_t* bytes, const uint64_t* excl, uint64_t n_excl, int64_t p,
-                                            uint64_t glo, int lane) {
+__device__ __noinline__ uint32_t chunk_tail_data(const uint4 d, const uint8_t* bytes, const uint64_t* excl,
+                                                 uint64_t n_excl, int64_t p, uint64_t glo, int lane) {
     CountArgs A{};
     A.bytes = bytes;
     A.excl = excl;
     A.n_excl = n_excl;
-    const int64_t b0 = p + 16 * lane;
-    uint4 d = make_uint4(0u, 0u, 0u, 0u);
-    if (b0 >= (int64_t)(glo & ~(uint64_t)15)) d = *(const uint4*)(A.bytes + b0);
     // first excluded interval that ends after the chunk start
     const uint64_t key = p < 0 ? 0 : (uint64_t)p;
     const uint64_t lo = wave_upper_bound(A.n_excl, key, lane, [&](uint64_t i) { return A.excl[2 * i + 1]; });
@@ -321,6 +327,14 @@ __device__ __noinline__ uint32_t chunk_tail(const uint8_t* bytes, const uint64_t
         if (lane >= dd) v = tail_combine<K>(o, v);
     }
     return (uint32_t)__builtin_amdgcn_readlane((int)v, kWave - 1);
+}
+
+// Inclusive tail of the 1 KiB chunk starting at p (warm-up only; p may lie
+// before glo or even before the buffer: those bytes read as invalid).
+template <int K>
+__device__ __forceinline__ uint32_t chunk_tail(const uint8_t* bytes, const uint64_t* excl, uint64_t n_excl, int64_t p,
+                                               uint64_t glo, int lane) {
+    return chunk_tail_data<K>(chunk_tail_load(bytes, p, glo, lane), bytes, excl, n_excl, p, glo, lane);
 }
 
 
@@ -354,6 +368,11 @@ struct Range {
         init(glo_, ghi_, lo_, hi_);
         warm<K>(A, lane);
     }
+    // Lane block of the chunk before c0 (the first warm-up step), so its load can
+    // be issued early; pass it to warm_from.
+    __device__ __forceinline__ uint4 ctx_load(const uint8_t* bytes, int lane) const {
+        return c0 > glo ? chunk_tail_load(bytes, (int64_t)c0 - kChunk, glo, lane) : make_uint4(0u, 0u, 0u, 0u);
+    }
     // Context and first interval (after init).
     template <int K>
     __device__ __forceinline__ void warm(const CountArgs& A, int lane) {
@@ -363,6 +382,24 @@ struct Range {
             p -= kChunk;
             carry = tail_combine<K>(chunk_tail<K>(A.bytes, A.excl, A.n_excl, p, glo, lane), carry);
         }
+        find_interval(A, lane);
+    }
+    // As warm, with the first chunk before c0 already loaded (ctx_load).
+    template <int K>
+    __device__ __forceinline__ void warm_from(const CountArgs& A, const uint4 dctx, int lane) {
+        carry = tail_pack(0, 0, 0);
+        int64_t p = (int64_t)c0;
+        if (p > (int64_t)glo) {
+            p -= kChunk;
+            carry = chunk_tail_data<K>(dctx, A.bytes, A.excl, A.n_excl, p, glo, lane);
+        }
+        for (; p > (int64_t)glo && !tail_complete<K>(carry);) {   // rare: a short chunk of context
+            p -= kChunk;
+            carry = tail_combine<K>(chunk_tail<K>(A.bytes, A.excl, A.n_excl, p, glo, lane), carry);
+        }
+        find_interval(A, lane);
+    }
+    __device__ __forceinline__ void find_interval(const CountArgs& A, int lane) {
         // first excluded interval ending after c0; its bounds live in registers so
         // the chunk loop issues no vector loads besides the byte stream (a VMEM load
         // there would force vmcnt(0) and drain the prefetch ring)

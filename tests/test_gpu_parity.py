@@ -332,3 +332,41 @@ def test_arbitrary_byte_values(torch_dev, oracle, k):
         blobs.append(head + a.tobytes())
     counts, totals = run_batch(blobs, k, torch_dev, fmt=1)
     check_against_oracle(oracle, blobs, k, counts, totals, fmt=1, tag="bytes")
+
+
+def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch):
+    """k=7 pair kernel: its u16 LDS counters overflow on low-complexity sequence
+    unless the drain path moves counts out exactly (poly-A, dinucleotide and
+    satellite repeats, N-broken poly-A that fills the unpaired-window table, and
+    FASTA lines of 1-7 bases that keep every chunk on the irregular path)."""
+    monkeypatch.setenv("KF_COUNT_VARIANT", "5")
+    rng = np.random.default_rng(4242)
+    sat = gen.random_seq(rng, 171).tobytes()
+    polya = b"A" * 40_000_000
+    blobs = [
+        b">polyA\n" + gen.wrap(np.frombuffer(polya, np.uint8), 80),
+        b">ac\n" + gen.wrap(np.frombuffer(b"AC" * 6_000_000, np.uint8), 60),
+        b">sat\n" + gen.wrap(np.frombuffer(sat * 60_000, np.uint8), 80),
+        b">nA\n" + (b"AAAAAAAAAN" * 1_500_000),
+        b">short\n" + gen.wrap(np.frombuffer(b"C" * 3_000_000, np.uint8), 7),
+        b">t\n" + gen.wrap(gen.random_seq(rng, 500_000), 80),
+    ]
+    counts, totals = run_batch(blobs, 7, torch_dev)
+    check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16")
+    # many genome pieces per workgroup, each above the drain threshold
+    blobs = [b">p\n" + gen.wrap(np.frombuffer(b"T" * int(rng.integers(60_000, 400_000)), np.uint8), 70)
+             for _ in range(300)]
+    counts, totals = run_batch(blobs, 7, torch_dev)
+    check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16-many")
+
+
+@pytest.mark.parametrize("variant", [5, 6, 7])
+def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
+    """k=7 pair kernel (KF_COUNT_VARIANT 5, 6, 7: prefetch ring 6 / 4 / 8) on ragged
+    FASTA, like the default forward-histogram kernel."""
+    monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
+    rng = np.random.default_rng(500 + variant)
+    blobs = [gen.random_fasta(rng, int(rng.integers(0, 300000)), max_records=5, n_rate=0.002, lower=0.05,
+                              crlf_rate=0.05, poly_rate=0.01) for _ in range(20)]
+    counts, totals = run_batch(blobs, 7, torch_dev)
+    check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"v{variant}")
