@@ -38,9 +38,12 @@ namespace kf {
 //   variant 1: 1024 threads (16 waves), 8 waves/SIMD register budget
 //   variant 2: as 1 with a 6-deep chunk prefetch ring (5 chunks in flight)
 //   variants 5..7: k = 7 pair counting (pair_kernel below), one 1024-thread
-//             workgroup per CU (160 KiB of LDS), 4 waves/SIMD, prefetch ring 6 / 4 / 8;
+//             workgroup per CU (144 KiB of LDS), 4 waves/SIMD, prefetch ring 6 / 4 / 8;
 //             for every other k they run as variant 1
-constexpr int kNumVariants = 8;
+//   variants 8, 9: k <= 7 dynamic-chunk forward histogram (dyn_kernel below), as
+//             variant 1 with chunks from an LDS counter, prefetch ring 4 / 6;
+//             for k = 8 they run as variant 1
+constexpr int kNumVariants = 10;
 constexpr int kDefaultVariant = 1;
 constexpr int kFirstPairVariant = 5;
 template <int V> struct Shape;
@@ -50,6 +53,8 @@ template <> struct Shape<2> { static constexpr int block = 1024, wpe = 8, abl = 
 template <> struct Shape<5> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 6; };
 template <> struct Shape<6> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 4; };
 template <> struct Shape<7> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 8; };
+template <> struct Shape<8> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 4; };
+template <> struct Shape<9> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 6; };
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
 template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 1, ring = 4; };   // no LDS adds
@@ -353,9 +358,24 @@ struct IvCursor {
     }
 };
 
+// Rare path: drain every hot word of P and S (one wave, CAS-exact as pair_drain).
+__device__ __noinline__ void pair_scan_drain(const uint32_t* __restrict__ code2col, uint32_t* gcounts, int lane) {
+    for (uint32_t w = (uint32_t)lane; w < kPairCtl / 4; w += kWave) {
+        const uint32_t v = __hip_atomic_load((lds_u32*)(uintptr_t)(4 * w), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (v & kU16Hot) pair_drain(4 * w, code2col, gcounts);
+    }
+}
+
+// The fast path checks the returned words of the PREVIOUS fast chunk (pend), after
+// issuing its own adds, so a wave never waits for its own LDS returns; a hot word
+// then costs one scan of P and S.  With that one chunk of delay at most three
+// chunks of adds per wave (16 x 3 x 520) land on a half between its crossing of
+// 0x4000 and the drain, still below 0x10000.
 template <bool MASKED>
 __device__ __forceinline__ void count_chunk_ind(const uint4 d, const CountArgs& A, const PPiece& P, uint32_t c,
-                                                int lane, uint64_t iv0, uint32_t* gcounts, uint32_t& lane_total) {
+                                                int lane, uint64_t iv0, uint32_t* gcounts, uint32_t& lane_total,
+                                                uint32_t (&pend)[9]) {
     constexpr int K = 7;
     const uint64_t own = P.c0 + (uint64_t)kOwn * c;
     if constexpr (!MASKED) {
@@ -386,7 +406,7 @@ __device__ __forceinline__ void count_chunk_ind(const uint4 d, const CountArgs& 
             auto paddr = [&](int j) -> uint32_t {
                 return (j == 0 ? (lo << 1) : __builtin_amdgcn_alignbit(hi, lo, 4 * j - 1)) & 0x1FFFCu;
             };
-            uint32_t o = 0;
+            uint32_t rt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             const bool single = lane == kWave - 1 && q;   // odd total: the newest window is unpaired
             if (lane != 0) {
 #pragma unroll
@@ -407,25 +427,22 @@ __device__ __forceinline__ void count_chunk_ind(const uint4 d, const CountArgs& 
 #elif KF_PAIR_ABL == 2   // profiling only: no pair adds at all
                     lane_total += paddr(j) ^ dl;
 #else
-                    o |= lds_add_rtn(paddr(j), dl);
+                    rt[j] = lds_add_rtn(paddr(j), dl);
 #endif
                 }
                 lane_total += nef;
                 if (single) {
                     const uint32_t y = C & 0x3FFFu;
                     const uint32_t i = s_fold(y, kf_revcomp<K>(y));
-                    o |= lds_add_rtn(s_addr(i), half_one(i));
+                    rt[8] = lds_add_rtn(s_addr(i), half_one(i));
                 }
             }
-            if (__builtin_amdgcn_ballot_w64((o & kU16Hot) != 0) != 0 && (o & kU16Hot)) {
-                // rare: some word this lane added to is hot; re-check all of them
+            uint32_t po = 0;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) pair_drain(paddr(j), A.code2col, gcounts);
-                if (single) {
-                    const uint32_t y = C & 0x3FFFu;
-                    pair_drain(s_addr(s_fold(y, kf_revcomp<K>(y))), A.code2col, gcounts);
-                }
-            }
+            for (int j = 0; j < 9; ++j) po |= pend[j];
+            if (__builtin_amdgcn_ballot_w64((po & kU16Hot) != 0) != 0) pair_scan_drain(A.code2col, gcounts, lane);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) pend[j] = rt[j];
             return;
         }
     }
@@ -467,10 +484,12 @@ __device__ __forceinline__ void count_chunk_ind(const uint4 d, const CountArgs& 
         const uint32_t i = s_fold(fwd(r), rcw(r));
         o |= lds_add_rtn(s_addr(i), ((R >> r) & 1u) * half_one(i));
     }
-    if (__builtin_amdgcn_ballot_w64((o & kU16Hot) != 0) != 0 && (o & kU16Hot)) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) pair_drain(s_addr(s_fold(fwd(r), rcw(r))), A.code2col, gcounts);
+    for (int j = 0; j < 9; ++j) {
+        o |= pend[j];
+        pend[j] = 0;
     }
+    if (__builtin_amdgcn_ballot_w64((o & kU16Hot) != 0) != 0) pair_scan_drain(A.code2col, gcounts, lane);
     lane_total += (uint32_t)__builtin_popcount(R);
 }
 
@@ -650,6 +669,9 @@ __global__ void __launch_bounds__(Shape<V>::block)
         atomicMax(A.prof + 43, (unsigned long long)rt1);
         atomicMax(A.prof + 44, (unsigned long long)(rt1 - rt0));
         atomicMax(A.prof + 45, (unsigned long long)rt0);
+        const int hb = blockIdx.x * 2 >= gridDim.x;
+        atomicAdd(A.prof + 46 + hb, (unsigned long long)(rt1 - rt0));
+        atomicMax(A.prof + 48 + hb, (unsigned long long)(rt1 - rt0));
     }
 }
 
@@ -735,6 +757,7 @@ __global__ void __launch_bounds__(Shape<V>::block) __attribute__((amdgpu_waves_p
         const uint32_t ctr = kPairCtl + 4 * par;
         uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
         uint32_t lt = 0, nproc = 0;
+        uint32_t pend[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // returns of the last fast chunk
         for (;;) {
 #pragma unroll
             for (int j = 0; j < RING; ++j) {
@@ -749,9 +772,9 @@ __global__ void __launch_bounds__(Shape<V>::block) __attribute__((amdgpu_waves_p
                     (void)msk;
 #else
                     if (msk)
-                        count_chunk_ind<true>(buf[j], A, P, c, lane, cur.iv, gc, lt);
+                        count_chunk_ind<true>(buf[j], A, P, c, lane, cur.iv, gc, lt, pend);
                     else
-                        count_chunk_ind<false>(buf[j], A, P, c, lane, cur.iv, gc, lt);
+                        count_chunk_ind<false>(buf[j], A, P, c, lane, cur.iv, gc, lt, pend);
 #endif
                     ++nproc;
                 }
@@ -844,6 +867,191 @@ __global__ void __launch_bounds__(Shape<V>::block) __attribute__((amdgpu_waves_p
         P = Pn;
         cur.load(A, P);   // re-base the interval cursor on the new piece
         par ^= 1u;
+    }
+}
+
+// ---------------------------------------------------------------- k <= 7 dynamic-chunk kernel
+// count_kernel's forward histogram (4^k u32 in LDS, two 1024-thread workgroups
+// per CU) fed like the pair kernel: self-contained chunks (lane 0 = context)
+// taken from an LDS counter.  The waves of a workgroup then finish a genome piece
+// together instead of the flush waiting for the slowest SIMD slot (a static
+// split left the oldest waves idle ~35 % of a piece), and no wave range needs a
+// warm-up.
+
+// Exact context before lane 1 of an irregular chunk whose lane-0 block B has tail
+// own_t (lane 0's value): empty when that block is complete on its own, else the
+// tail of the bytes before B (walk back, rare).
+template <int K>
+__device__ __forceinline__ uint32_t chunk_context(const CountArgs& A, const PPiece& P, uint64_t B, uint32_t own_t,
+                                                  int lane) {
+    uint32_t carry = tail_pack(0, 0, 0);
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)own_t, 0);
+    if (!tail_complete<K>(t0)) {
+        for (int64_t p = (int64_t)B; p > (int64_t)P.glo && !tail_complete<K>(carry);) {
+            p -= kChunk;
+            carry = tail_combine<K>(chunk_tail<K>(A.bytes, A.excl, A.n_excl, p, P.glo, lane), carry);
+        }
+    }
+    return carry;
+}
+
+template <int K, bool MASKED>
+__device__ __forceinline__ void count_chunk_fwd(const uint4 d, const CountArgs& A, const PPiece& P, uint32_t c,
+                                                int lane, uint64_t iv0, uint32_t& lane_total) {
+    constexpr uint32_t M4 = ((1u << (2 * K)) - 1u) << 2;
+    if constexpr (!MASKED) {
+        uint32_t Cf, NNL, bad;
+        classify16_fast(d, Cf, NNL, bad);
+        const uint32_t nef = (uint32_t)__builtin_popcount(NNL);
+        const bool self_ok = bad == 0 && nef >= 15u;
+        if (__builtin_amdgcn_ballot_w64(!self_ok) == 0) {
+            // as count_chunk's fast case; lane 0's 15-16 bases are lane 1's context
+            const uint32_t r = (uint32_t)__builtin_ctz((NNL ^ 0xFFFFu) | 0x10000u);
+            const uint32_t lo1 = (1u << r) - 1u, lo2 = lo1 | (lo1 << r);
+            const uint32_t C = bfi(lo2, Cf, Cf >> 2);
+            const uint32_t pC = wave_shr1(0u, C);
+            const uint32_t xlo = C << 2, xhi = (pC << ((2u * nef + 2u) & 31u)) | (C >> 30);
+            uint32_t xv[8];
+#pragma unroll
+            for (int o = 0; o < 8; ++o) xv[o] = o ? __builtin_amdgcn_alignbit(xhi, xlo, 2 * o) : xlo;
+            auto addr = [&](int w) -> uint32_t { return (w < 8 ? xv[w] : (xv[w - 8] >> 16)) & M4; };
+            if (lane != 0) {
+                const uint32_t inc15 = nef >> 4;   // window 15 exists iff no newline
+#pragma unroll
+                for (int w = 0; w < 15; ++w) lds_add(addr(w), 1u);
+                lds_add(addr(15), inc15);
+                lane_total += 15u + inc15;
+            }
+            return;
+        }
+    }
+    const uint64_t own = P.c0 + (uint64_t)kOwn * c;
+    const uint64_t B = own - 16;   // lane 0's block (may lie before the genome: invalid)
+    const ChunkMask m{P.glo, max(own, P.plo), min(own + kOwn, P.phi)};
+    uint32_t C, V, EN, ne, own_t;
+    front_end<K, true>(d, A, B, lane, m, iv0, C, V, EN, ne, own_t);
+    const Windows win = windows<K, true>(C, V, EN, ne, chunk_context<K>(A, P, B, own_t, lane), lane);
+    const uint32_t xlo = win.wlo << 2, xhi = __builtin_amdgcn_alignbit(win.whi, win.wlo, 30);
+    uint32_t xv[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) xv[o] = o ? __builtin_amdgcn_alignbit(xhi, xlo, 2 * o) : xlo;
+    auto addr = [&](int r) -> uint32_t { return (r < 8 ? xv[r] : (xv[r - 8] >> 16)) & M4; };
+#pragma unroll
+    for (int r = 0; r < 16; ++r) lds_add(addr(r), (win.R >> r) & 1u);
+    lane_total += (uint32_t)__builtin_popcount(win.R);
+}
+
+template <int K, int V>
+__global__ void __launch_bounds__(Shape<V>::block) __attribute__((amdgpu_waves_per_eu(Shape<V>::wpe, Shape<V>::wpe)))
+    dyn_kernel(CountArgs A) {
+    constexpr int kBlock = Shape<V>::block;
+    constexpr int RING = Shape<V>::ring;
+    constexpr uint32_t NCODES = 1u << (2 * K);
+    constexpr uint32_t CTL = NCODES * 4;   // byte address of the chunk counter
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (uint32_t i = tid; i < NCODES + 4; i += kBlock) hist[i] = 0;
+    __syncthreads();
+    if ((uint32_t)(uintptr_t)(lds_u32*)hist != 0u) __builtin_trap();   // addresses assume LDS base 0
+
+    const uint64_t base = A.goff[0];
+    const uint64_t total = A.goff[A.n_genomes] - base;
+    const uint64_t G = gridDim.x, b = blockIdx.x;
+    const uint64_t span_lo = base + ((total / G * b + (total % G) * b / G) & ~(uint64_t)15);
+    const uint64_t span_hi = (b + 1 == G) ? base + total
+                                          : base + ((total / G * (b + 1) + (total % G) * (b + 1) / G) & ~(uint64_t)15);
+    if (span_lo >= span_hi) return;
+    const uint64_t tk0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t rt0 = A.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, span_lo, lane,
+                                          [&](uint64_t i) { return A.goff[i + 1]; });
+    PPiece P;
+    g = pair_next_piece(A, g, span_lo, span_hi, P);
+    IvCursor cur;
+    cur.init(A, P.c0 >= 16 ? P.c0 - 16 : 0, lane);
+    while (g < A.n_genomes) {
+        cur.load(A, P);
+        const uint64_t t0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+        uint32_t idx[RING];
+        uint4 buf[RING];
+#pragma unroll
+        for (int j = 0; j < RING; ++j) {
+            idx[j] = __builtin_amdgcn_readfirstlane(pair_grab(CTL, lane));
+            buf[j] = pload(P, idx[j], lane);
+        }
+        uint32_t lt = 0, nproc = 0;
+        for (;;) {
+#pragma unroll
+            for (int j = 0; j < RING; ++j) {
+                const uint32_t tok = pair_grab(CTL, lane);   // refill of this slot, used below
+                const uint32_t c = idx[j];
+                if (c < P.nch) {
+                    const uint32_t own_r = kOwn * c;
+                    const bool msk = own_r < P.fast_lo || own_r + kOwn > P.fast_hi ||
+                                     cur.hits(A, P, own_r, own_r + kChunk);
+                    if (msk)
+                        count_chunk_fwd<K, true>(buf[j], A, P, c, lane, cur.iv, lt);
+                    else
+                        count_chunk_fwd<K, false>(buf[j], A, P, c, lane, cur.iv, lt);
+                    ++nproc;
+                }
+                idx[j] = __builtin_amdgcn_readfirstlane(tok);
+                buf[j] = pload(P, idx[j], lane);
+            }
+            uint32_t mn = idx[0];
+#pragma unroll
+            for (int j = 1; j < RING; ++j) mn = min(mn, idx[j]);
+            if (mn >= P.nch) break;
+        }
+        const unsigned long long s = wave_sum(lt);
+        if (lane == 0 && s) atomicAdd(A.totals + g, s);
+        const uint64_t t1 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+        if (A.prof && lane == 0) {
+            atomicAdd(A.prof + 1, (unsigned long long)(t1 - t0));
+            atomicAdd(A.prof + 2, 1ull);
+            atomicAdd(A.prof + 8 + wave, (unsigned long long)(t1 - t0));
+            atomicAdd(A.prof + 24 + wave, (unsigned long long)nproc);
+        }
+        __syncthreads();
+        const uint64_t t_f1 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+        // canonical bin = forward count of the k-mer + forward count of its revcomp;
+        // coalesced u32 atomics in column order, histogram re-zeroed on the way
+        uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
+        for (uint32_t col = tid; col < A.nbins; col += kBlock) {
+            const uint32_t rep = A.col2rep[col];
+            const uint32_t rc = kf_revcomp<K>(rep);
+            const uint32_t v = hist[rep] + (rc != rep ? hist[rc] : 0u);
+            if (v) {
+                hist[rep] = 0;
+                hist[rc] = 0;
+                __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (tid == 0) hist[NCODES] = 0;   // the chunk counter
+        const uint64_t t_f2 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+        __syncthreads();
+        if (A.prof && tid == 0) {
+            const uint64_t t_f3 = __builtin_amdgcn_s_memtime();
+            atomicAdd(A.prof + 3, (unsigned long long)(t_f1 - t1));
+            atomicAdd(A.prof + 4, 1ull);
+            atomicAdd(A.prof + 5, (unsigned long long)(t_f2 - t_f1));
+            atomicAdd(A.prof + 6, (unsigned long long)(t_f3 - t_f2));
+        }
+        g = pair_next_piece(A, g + 1, span_lo, span_hi, P);
+    }
+    if (A.prof && tid == 0) {
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(A.prof + 40, (unsigned long long)(__builtin_amdgcn_s_memtime() - tk0));
+        atomicAdd(A.prof + 41, (unsigned long long)(rt1 - rt0));
+        atomicMin(A.prof + 42, (unsigned long long)rt0);
+        atomicMax(A.prof + 43, (unsigned long long)rt1);
+        atomicMax(A.prof + 44, (unsigned long long)(rt1 - rt0));
+        atomicMax(A.prof + 45, (unsigned long long)rt0);
+        const int hb = blockIdx.x * 2 >= gridDim.x;
+        atomicAdd(A.prof + 46 + hb, (unsigned long long)(rt1 - rt0));
+        atomicMax(A.prof + 48 + hb, (unsigned long long)(rt1 - rt0));
     }
 }
 
@@ -982,8 +1190,22 @@ void* count_kernel_v(int k) {
 }
 
 // Variants >= kFirstPairVariant are the pair kernel at k = 7 and variant 1 elsewhere.
-bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant; }
-int effective_variant(int k, int v) { return (v >= kFirstPairVariant && !is_pair(k, v)) ? 1 : v; }
+bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant && v <= 7; }
+bool is_dyn(int k, int v) { return k <= kLdsMaxK && (v == 8 || v == 9); }
+int effective_variant(int k, int v) { return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v)) ? 1 : v; }
+
+template <int V>
+void* dyn_kernel_v(int k) {
+    switch (k) {
+    case 2: return (void*)&dyn_kernel<2, V>;
+    case 3: return (void*)&dyn_kernel<3, V>;
+    case 4: return (void*)&dyn_kernel<4, V>;
+    case 5: return (void*)&dyn_kernel<5, V>;
+    case 6: return (void*)&dyn_kernel<6, V>;
+    case 7: return (void*)&dyn_kernel<7, V>;
+    default: return nullptr;
+    }
+}
 
 void* count_kernel_for(int k, int v) {
     if (is_pair(k, v)) {
@@ -991,6 +1213,7 @@ void* count_kernel_for(int k, int v) {
         if (v == 7) return (void*)&pair_kernel<7>;
         return (void*)&pair_kernel<5>;
     }
+    if (is_dyn(k, v)) return v == 9 ? dyn_kernel_v<9>(k) : dyn_kernel_v<8>(k);
     v = effective_variant(k, v);
 #ifdef KF_ABLATION
     if (v == 3) return count_kernel_v<3>(k);
@@ -1023,6 +1246,7 @@ int current_variant() {
 // kernel: P + S, nothing else
 int lds_bytes_for(int k, int v) {
     if (is_pair(k, v)) return (int)kPairLdsBytes;
+    if (is_dyn(k, v)) return (int)(sizeof(uint32_t) << (2 * k)) + 16;
     if (k <= kLdsMaxK) return (int)(sizeof(uint32_t) << (2 * k)) + 16 * 8;
     if (k <= kMultiMaxK) return (int)(sizeof(uint32_t) << kMultiBits) + 16 * 8;
     return 0;
@@ -1052,6 +1276,9 @@ int launch_info(int k, int* grid, int* block, int* lds, int* variant) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return kf_fail(KF_EHIP, "hipDeviceGetAttribute(MultiprocessorCount) failed");
         if (per_cu < 1) per_cu = 1;
+        // measurement knob: at most N workgroups per CU (dynamic-chunk kernels)
+        const char* e = getenv("KF_WGS_PER_CU");
+        if (e && atoi(e) >= 1 && atoi(e) < per_cu && is_dyn(k, v)) per_cu = atoi(e);
         gr = per_cu * cus;
     }
     *grid = gr;
@@ -1103,7 +1330,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.prof = nullptr;
     const char* pe = getenv("KF_COUNT_PROFILE");   // debugging aid: synchronous, prints to stderr
     if (pe && *pe == '1' && !bucket) {
-        if (hipMalloc((void**)&A.prof, 48 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 48 * 8, s) != hipSuccess ||
+        if (hipMalloc((void**)&A.prof, 56 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 56 * 8, s) != hipSuccess ||
             hipMemsetAsync(A.prof + 42, 0xFF, 8, s) != hipSuccess)
             return kf_fail(KF_EHIP, "profile buffer");
     }
@@ -1119,7 +1346,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (A.prof) {
-        unsigned long long h[48];
+        unsigned long long h[56];
         float ms = 0.f;
         if (hipEventRecord(pe1, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess ||
             hipEventElapsedTime(&ms, pe0, pe1) != hipSuccess ||
@@ -1130,6 +1357,9 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
         fprintf(stderr, "  kernel %.3f ms (events); workgroup lifetime mean %.3f max %.3f ms; first start to "
                 "last end %.3f ms, last start %.3f ms after the first\n", ms, (double)h[41] / (double)grid * 1e-5,
                 (double)h[44] * 1e-5, (double)(h[43] - h[42]) * 1e-5, (double)(h[45] - h[42]) * 1e-5);
+        fprintf(stderr, "  first half of the grid: mean %.3f max %.3f ms; second half: mean %.3f max %.3f ms\n",
+                (double)h[46] / (double)(grid / 2) * 1e-5, (double)h[48] * 1e-5,
+                (double)h[47] / (double)(grid - grid / 2) * 1e-5, (double)h[49] * 1e-5);
         (void)hipFree(A.prof);
         const double nf = h[4] ? (double)h[4] : 1.0, nr = h[2] ? (double)h[2] : 1.0;
         fprintf(stderr, "[count_kernel k=%d] wave ranges %llu: setup %.3g cyc/range, loop %.3g cyc/range; "

@@ -289,11 +289,11 @@ def test_bucket_kernel_agrees_with_other_large_k_paths(torch_dev, monkeypatch, k
     assert torch.equal(out[9][0], out[13][0]) and torch.equal(out[9][1], out[13][1])
 
 
-@pytest.mark.parametrize("variant", [0, 2])
-@pytest.mark.parametrize("k", [5, 7, 8])
+@pytest.mark.parametrize("variant", [0, 2, 8, 9])
+@pytest.mark.parametrize("k", [3, 5, 7, 8])
 def test_count_kernel_variants_match_oracle(torch_dev, oracle, monkeypatch, variant, k):
-    """The other workgroup shapes of the count kernel (KF_COUNT_VARIANT: 512-thread,
-    6-deep prefetch ring) on ragged FASTA."""
+    """The other shapes of the count kernel (KF_COUNT_VARIANT: 512-thread, 6-deep
+    prefetch ring, dynamic-chunk kernels with 4- and 6-deep rings) on ragged FASTA."""
     monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
     rng = np.random.default_rng(300 + 10 * variant + k)
     blobs = [gen.random_fasta(rng, int(rng.integers(0, 200000)), max_records=5, n_rate=0.002, lower=0.05,
