@@ -118,9 +118,14 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
             for (int o = 0; o < 8; ++o) xv[o] = o ? __builtin_amdgcn_alignbit(xhi, xlo, 2 * o) : xlo;
             auto addr = [&](int w) -> uint32_t { return (w < 8 ? xv[w] : (xv[w - 8] >> 16)) & M4; };
             const uint32_t inc15 = nef >> 4;   // window 15 exists iff no newline
+#ifdef KF_K1_NOADD   // profiling only (tools/build_abl.sh): the fast path without its LDS adds
+#pragma unroll
+            for (int w = 0; w < 16; ++w) lane_total += addr(w);
+#else
 #pragma unroll
             for (int w = 0; w < 15; ++w) lds_add(addr(w), 1u);
             lds_add(addr(15), inc15);
+#endif
             lane_total += 15u + inc15;
             // lane 63's block is all valid bases: its tail is complete
             const uint32_t c63 = (uint32_t)__builtin_amdgcn_readlane((int)C, kWave - 1);
