@@ -87,7 +87,9 @@ __device__ __forceinline__ void classify16(const uint4 d, uint32_t& C, uint32_t&
 }
 
 // Fast-path flavour of classify16: codes C, not-newline mask NNL, and `bad`,
-// non-zero iff some byte is neither a base nor a newline (OR of vf & nf).
+// non-zero iff some byte is neither a base nor a newline: z = (b ^ TBL[cb]) & 0xDF
+// with TBL = "ACTG" is 0 exactly for a base (either case), and newline bytes are
+// masked out by nf (one v_perm per word less than testing z with a v_perm).
 __device__ __forceinline__ void classify16_fast(const uint4 d, uint32_t& C, uint32_t& NNL, uint32_t& bad) {
     const uint32_t w[4] = {d.x, d.y, d.z, d.w};
     uint32_t pc[4], nf[4];
@@ -96,11 +98,10 @@ __device__ __forceinline__ void classify16_fast(const uint4 d, uint32_t& C, uint
     for (int q = 0; q < 4; ++q) {
         const uint32_t x = w[q];
         const uint32_t cb = (x >> 1) & 0x03030303u;
-        const uint32_t ex = __builtin_amdgcn_perm(0u, 0x4B584F4Du, cb);
-        const uint32_t y = (x ^ ex) & 0xDFDFDFDFu;
-        const uint32_t vf = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, y);
+        const uint32_t ex = __builtin_amdgcn_perm(0u, 0x47544341u, cb);   // "ACTG"
+        const uint32_t z = (x ^ ex) & 0xDFDFDFDFu;
         nf[q] = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, x ^ 0x06060606u);
-        bad |= vf & nf[q];
+        bad |= z & nf[q];
         pc[q] = __builtin_amdgcn_udot4(cb, 0x01041040u, 0u, false);
     }
     const uint32_t c01 = __builtin_amdgcn_perm(pc[0], pc[1], 0x0C0C0400u);
