@@ -46,13 +46,18 @@ namespace kf {
 constexpr int kNumVariants = 10;
 constexpr int kDefaultVariant = 1;
 constexpr int kFirstPairVariant = 5;
+#ifndef KF_PAIR_ABL
+#define KF_PAIR_ABL 0
+#endif
+// pair variants: 4 waves/SIMD (one workgroup per CU); the half-table ablation runs two
+constexpr int kPairWpe = KF_PAIR_ABL == 4 ? 8 : 4;
 template <int V> struct Shape;
 template <> struct Shape<0> { static constexpr int block = 512, wpe = 0, abl = 0, ring = 4; };
 template <> struct Shape<1> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 4; };
 template <> struct Shape<2> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 6; };
-template <> struct Shape<5> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 6; };
-template <> struct Shape<6> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 4; };
-template <> struct Shape<7> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 8; };
+template <> struct Shape<5> { static constexpr int block = 1024, wpe = kPairWpe, abl = 0, ring = 6; };
+template <> struct Shape<6> { static constexpr int block = 1024, wpe = kPairWpe, abl = 0, ring = 4; };
+template <> struct Shape<7> { static constexpr int block = 1024, wpe = kPairWpe, abl = 0, ring = 8; };
 template <> struct Shape<8> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 4; };
 template <> struct Shape<9> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 6; };
 #ifdef KF_ABLATION
@@ -209,13 +214,18 @@ __device__ __forceinline__ uint32_t count_chunk(const uint4 d, const CountArgs& 
 // moved to the genome's count row (pair_drain).  At most two chunks of adds per
 // wave (16 waves x 2 x 1024) can land on a half between its crossing and the
 // first drain, so it stays below 0x4000 + 0x8000: the counts are exact.
+#if KF_PAIR_ABL == 4   // profiling only: P folded to 64 KiB and S to 8 KiB (wrong counts), 2 workgroups/CU
+constexpr uint32_t kPairSBase = 1u << 16;
+constexpr uint32_t kPairCtl = kPairSBase + (1u << 13);
+#else
 constexpr uint32_t kPairSBase = 1u << 17;                    // byte offset of S
 constexpr uint32_t kPairCtl = kPairSBase + (1u << 14);       // two chunk counters (pair_kernel)
+#endif
 constexpr uint32_t kPairLdsBytes = kPairCtl + 16;
 constexpr uint32_t kU16Hot = 0xC000C000u;                    // a half >= 0x4000
-#ifndef KF_PAIR_ABL
-#define KF_PAIR_ABL 0
-#endif
+// (address masks: no-ops for the real layout, keep the ablation inside its LDS)
+constexpr uint32_t kPairPMask = kPairSBase - 4u;
+constexpr uint32_t kPairSMask = kPairCtl - kPairSBase - 4u;
 
 __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
     return __hip_atomic_fetch_add((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -228,7 +238,7 @@ __device__ __forceinline__ uint32_t s_fold(uint32_t y, uint32_t rc) {
     return ((z >> 8) << 7) | (z & 0x7Fu);
 }
 __device__ __forceinline__ uint32_t s_unfold(uint32_t i) { return ((i >> 7) << 8) | (i & 0x7Fu); }
-__device__ __forceinline__ uint32_t s_addr(uint32_t i) { return kPairSBase + ((i >> 1) << 2); }
+__device__ __forceinline__ uint32_t s_addr(uint32_t i) { return kPairSBase + (((i >> 1) << 2) & kPairSMask); }
 __device__ __forceinline__ uint32_t half_one(uint32_t i) { return 1u << ((i & 1u) << 4); }
 
 // Rare path: move 0x4000 out of each half of the LDS word at byte address a that
@@ -409,7 +419,7 @@ __device__ __forceinline__ void count_chunk_ind(const uint4 d, const CountArgs& 
             const uint32_t one = 1u;
             const bool has7 = !(nef == 15u && p == 0u);   // pair 7 would end at entry 15
             auto paddr = [&](int j) -> uint32_t {
-                return (j == 0 ? (lo << 1) : __builtin_amdgcn_alignbit(hi, lo, 4 * j - 1)) & 0x1FFFCu;
+                return (j == 0 ? (lo << 1) : __builtin_amdgcn_alignbit(hi, lo, 4 * j - 1)) & kPairPMask;
             };
             uint32_t rt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             const bool single = lane == kWave - 1 && q;   // odd total: the newest window is unpaired
@@ -427,7 +437,7 @@ __device__ __forceinline__ void count_chunk_ind(const uint4 d, const CountArgs& 
                     case 6: dl = shl1_byte<3>(H0, one); break;
                     default: dl = has7 ? shl1_byte<3>(H1, one) : 0u; break;
                     }
-#if KF_PAIR_ABL == 1   // profiling only: no returns, no overflow check (wrong on low complexity)
+#if KF_PAIR_ABL == 1 || KF_PAIR_ABL == 4   // profiling only: no returns, no overflow check (wrong on low complexity)
                     lds_add(paddr(j), dl);
 #elif KF_PAIR_ABL == 2   // profiling only: no pair adds at all
                     lane_total += paddr(j) ^ dl;
@@ -815,12 +825,12 @@ __global__ void __launch_bounds__(Shape<V>::block) __attribute__((amdgpu_waves_p
         uint32_t F[16];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const uint4 w = h4[i * 1024 + tid];   // words 2y .. 2y+3 of y = 2048 i + 2 tid
+            const uint4 w = h4[(i * 1024 + tid) & (kPairSBase / 16 - 1)];   // words 2y .. 2y+3 of y = 2048 i + 2 tid
             F[2 * i] = u16sum2(w.x) + u16sum2(w.y);
             F[2 * i + 1] = u16sum2(w.z) + u16sum2(w.w);
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                const uint32_t v = hist[a * 8192 + i * 1024 + tid];   // halves a 4^7 + y, a 4^7 + y + 1
+                const uint32_t v = hist[(a * 8192 + i * 1024 + tid) & (kPairSBase / 4 - 1)];   // halves a 4^7 + y, a 4^7 + y + 1
                 F[2 * i] += v & 0xFFFFu;
                 F[2 * i + 1] += v >> 16;
             }
@@ -842,7 +852,7 @@ __global__ void __launch_bounds__(Shape<V>::block) __attribute__((amdgpu_waves_p
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const uint32_t y = rep[c], rc = kf_revcomp<K>(y);
-            const uint32_t v = hist[y] + hist[rc] + S[s_fold(y, rc)];
+            const uint32_t v = hist[y] + hist[rc] + S[s_fold(y, rc) & ((kPairCtl - kPairSBase) / 2 - 1)];
             if (v) __hip_atomic_fetch_add(gcf + tid + c * kBlock, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();   // (D) columns read
