@@ -83,6 +83,7 @@ struct BucketArgs {
     uint16_t* meta;            // gridDim.x * (nbk+1) * kRmax round bucket offsets
     uint32_t* roff;            // gridDim.x * kRmax round record offsets
     uint32_t accumulate;
+    uint32_t slot_w;            // phase-2 rounds per wave by wave slot (4 x 8 bit, see bucket_weights)
     unsigned long long* prof;   // optional (KF_BUCKET_PROFILE): per-workgroup phase cycles
 };
 
@@ -352,10 +353,21 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         // wave, typically); the next bucket's first group is issued before this
         // bucket's flush, so its loads are in flight during the flush.  Loads are
         // unconditional (inactive lanes read unit 0) so vmcnt stays exact.
-        const uint32_t myr = (uint32_t)wave + kBkWaves * (uint32_t)lane;
+        // Rounds are dealt to waves in patterns of 4 (a0 + a1 + a2 + a3) rounds, a_s
+        // consecutive rounds to each wave of slot s = wave >> 2 (its age on its
+        // SIMD: older slots issue first and finish sooner, so they may take more);
+        // a = 1,1,1,1 is round wave + 16 j.  The valid runs are lanes 0 .. nrun-1.
+        const uint32_t slot = (uint32_t)wave >> 2;
+        const uint32_t a_s = (B.slot_w >> (8 * slot)) & 0xFFu;
+        const uint32_t a_below = ((B.slot_w & 0xFFu) * (slot > 0)) + (((B.slot_w >> 8) & 0xFFu) * (slot > 1)) +
+                                 (((B.slot_w >> 16) & 0xFFu) * (slot > 2));
+        const uint32_t per = 4 * ((B.slot_w & 0xFFu) + ((B.slot_w >> 8) & 0xFFu) + ((B.slot_w >> 16) & 0xFFu) +
+                                  (B.slot_w >> 24));
+        const uint32_t lq = (uint32_t)lane / a_s;
+        const uint32_t myr = lq * per + 4 * a_below + ((uint32_t)wave & 3u) * a_s + ((uint32_t)lane - lq * a_s);
         const bool myr_ok = myr < nround;
         const uint32_t myr_c = myr_ok ? myr : 0u;
-        const uint32_t nrun = nround > (uint32_t)wave ? (nround - (uint32_t)wave + kBkWaves - 1) / kBkWaves : 0u;
+        const uint32_t nrun = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(myr_ok));
         const uint32_t ro_l = __builtin_nontemporal_load(roff + myr_c);
         const uint32_t ro = myr_ok ? ro_l : 0u;
         // raw (lanes without a run read round 0; make_tbl masks them), so that
@@ -574,6 +586,25 @@ uint32_t bucket_lds_for(int k) {
     }
 }
 
+// Phase-2 rounds per wave by wave slot, packed 4 x 8 bit (slot 0 in the low byte).
+// KF_BK_WEIGHTS="a0,a1,a2,a3" (tuning/A-B knob, read per launch), each 1..32; a set
+// that could give a wave more than 64 runs of a piece is refused (default used).
+uint32_t bucket_weights() {
+    constexpr uint32_t kDefault = 0x01010101u;
+    const char* e = getenv("KF_BK_WEIGHTS");
+    if (!e || !*e) return kDefault;
+    unsigned a[4];
+    if (sscanf(e, "%u,%u,%u,%u", &a[0], &a[1], &a[2], &a[3]) != 4) return kDefault;
+    uint32_t per = 0, amax = 0;
+    for (int i = 0; i < 4; ++i) {
+        if (a[i] < 1 || a[i] > 32) return kDefault;
+        per += 4 * a[i];
+        amax = a[i] > amax ? a[i] : amax;
+    }
+    if ((kRmax / per + 1) * amax > (uint32_t)kWave) return kDefault;
+    return a[0] | a[1] << 8 | a[2] << 16 | a[3] << 24;
+}
+
 // Per-device state: bucket tables per k and the scratch of the last launch
 // size.  A launch on another stream waits for the previous user of the scratch.
 struct DevState {
@@ -692,6 +723,7 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     B.meta = (uint16_t*)((char*)d.scratch + rec_b);
     B.roff = (uint32_t*)((char*)d.scratch + rec_b + meta_b);
     B.accumulate = (flags & KF_ACCUMULATE) ? 1u : 0u;
+    B.slot_w = bucket_weights();
     B.prof = nullptr;
     const char* pe = getenv("KF_BUCKET_PROFILE");   // debugging aid: synchronous, prints to stderr
     std::vector<unsigned long long> prof_h;
