@@ -43,7 +43,10 @@ namespace kf {
 //   variants 8, 9: k <= 7 dynamic-chunk forward histogram (dyn_kernel below), as
 //             variant 1 with chunks from an LDS counter, prefetch ring 4 / 6;
 //             for k = 8 they run as variant 1
-constexpr int kNumVariants = 10;
+//   variants 10, 11: k = 7 pair counting on count_kernel's static wave ranges
+//             (count_chunk_pair), one 1024-thread workgroup per CU, ring 6 / 8;
+//             for every other k they run as variant 1
+constexpr int kNumVariants = 12;
 constexpr int kDefaultVariant = 1;
 constexpr int kFirstPairVariant = 5;
 #ifndef KF_PAIR_ABL
@@ -60,6 +63,9 @@ template <> struct Shape<6> { static constexpr int block = 1024, wpe = kPairWpe,
 template <> struct Shape<7> { static constexpr int block = 1024, wpe = kPairWpe, abl = 0, ring = 8; };
 template <> struct Shape<8> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 4; };
 template <> struct Shape<9> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 6; };
+template <> struct Shape<10> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 6; };
+template <> struct Shape<11> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 8; };
+template <int V> constexpr bool kStaticPair = V == 10 || V == 11;
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
 template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 1, ring = 4; };   // no LDS adds
@@ -382,6 +388,64 @@ __device__ __noinline__ void pair_scan_drain(const uint32_t* __restrict__ code2c
     }
 }
 
+__device__ __forceinline__ uint32_t u16sum2(uint32_t w) { return (w & 0xFFFFu) + (w >> 16); }
+
+// Flush step 1 (1024 threads): per forward 7-mer y, F(y) = sum_a P[4y + a] +
+// sum_a P[a 4^7 + y]; thread t owns y = 2048 i + 2t + {0, 1}, i = 0..7
+// (lane-consecutive reads).
+__device__ __forceinline__ void pair_f_sums(const uint32_t* hist, int tid, uint32_t (&F)[16]) {
+    const uint4* h4 = (const uint4*)hist;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint4 w = h4[(i * 1024 + tid) & (kPairSBase / 16 - 1)];   // words 2y .. 2y+3 of y = 2048 i + 2 tid
+        F[2 * i] = u16sum2(w.x) + u16sum2(w.y);
+        F[2 * i + 1] = u16sum2(w.z) + u16sum2(w.w);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const uint32_t v = hist[(a * 8192 + i * 1024 + tid) & (kPairSBase / 4 - 1)];   // halves a 4^7 + y, a 4^7 + y + 1
+            F[2 * i] += v & 0xFFFFu;
+            F[2 * i + 1] += v >> 16;
+        }
+    }
+}
+
+// Every counted window of an irregular chunk as a single 7-mer into S; with
+// these returns the pending ones of the last fast chunk are checked too.
+__device__ __forceinline__ void pair_singles(const Windows& win, const CountArgs& A, uint32_t* gcounts, int lane,
+                                             uint32_t& lane_total, uint32_t (&pend)[9]) {
+    constexpr int K = 7;
+    const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
+    const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
+                            __builtin_amdgcn_alignbit(whi, wlo, 24)};
+    auto fwd = [&](int r) -> uint32_t {
+        const int fo = (2 * r) & ~7;
+        return __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, 2 * K);
+    };
+    // reverse complement of the 64-bit window: revcomp of window r = bits [2(15-r), +2K) of RP
+    const uint32_t rhi = revpairs(wlo) ^ 0xAAAAAAAAu, rlo = revpairs(whi) ^ 0xAAAAAAAAu;
+    constexpr int RS = 2 * (17 - K);
+    const uint32_t rplo = __builtin_amdgcn_alignbit(rhi, rlo, RS), rphi = rhi >> RS;
+    const uint32_t rv[4] = {rplo, __builtin_amdgcn_alignbit(rphi, rplo, 8), __builtin_amdgcn_alignbit(rphi, rplo, 16),
+                            __builtin_amdgcn_alignbit(rphi, rplo, 24)};
+    auto rcw = [&](int r) -> uint32_t {
+        const int rr = 2 * (15 - r), ro = rr & ~7;
+        return __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, 2 * K);
+    };
+    uint32_t o = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t i = s_fold(fwd(r), rcw(r));
+        o |= lds_add_rtn(s_addr(i), ((R >> r) & 1u) * half_one(i));
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        o |= pend[j];
+        pend[j] = 0;
+    }
+    if (__builtin_amdgcn_ballot_w64((o & kU16Hot) != 0) != 0) pair_scan_drain(A.code2col, gcounts, lane);
+    lane_total += (uint32_t)__builtin_popcount(R);
+}
+
 // The fast path checks the returned words of the PREVIOUS fast chunk (pend), after
 // issuing its own adds, so a wave never waits for its own LDS returns; a hot word
 // then costs one scan of P and S.  With that one chunk of delay at most three
@@ -476,45 +540,101 @@ __device__ __forceinline__ void count_chunk_ind(const uint4 d, const CountArgs& 
         }
     }
     const Windows win = windows<K, true>(C, V, EN, ne, carry, lane);
-    const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
-    const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
-                            __builtin_amdgcn_alignbit(whi, wlo, 24)};
-    auto fwd = [&](int r) -> uint32_t {
-        const int fo = (2 * r) & ~7;
-        return __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, 2 * K);
-    };
-    // reverse complement of the 64-bit window: revcomp of window r = bits [2(15-r), +2K) of RP
-    const uint32_t rhi = revpairs(wlo) ^ 0xAAAAAAAAu, rlo = revpairs(whi) ^ 0xAAAAAAAAu;
-    constexpr int RS = 2 * (17 - K);
-    const uint32_t rplo = __builtin_amdgcn_alignbit(rhi, rlo, RS), rphi = rhi >> RS;
-    const uint32_t rv[4] = {rplo, __builtin_amdgcn_alignbit(rphi, rplo, 8), __builtin_amdgcn_alignbit(rphi, rplo, 16),
-                            __builtin_amdgcn_alignbit(rphi, rplo, 24)};
-    auto rcw = [&](int r) -> uint32_t {
-        const int rr = 2 * (15 - r), ro = rr & ~7;
-        return __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, 2 * K);
-    };
-    uint32_t o = 0;
+    pair_singles(win, A, gcounts, lane, lane_total, pend);
+}
+
+// Pair counting on count_kernel's static wave ranges (variants 10, 11): a chunk
+// continues its wave's stream (lane 0's context is the carry), so every lane of
+// the fast case holds 16 windows (8 pairs) or, with a newline in its block, 15
+// (7 pairs and its oldest window as a single).  Irregular chunks go to S whole.
+// Returns are checked one chunk late as in count_chunk_ind: this chunk's land in
+// pout, the previous chunk's are checked from pin.  The caller alternates two
+// register sets by ring-slot parity, so no returned word is ever copied (a copy
+// would wait for the returns before this chunk's adds go out).
+template <bool MASKED>
+__device__ __forceinline__ uint32_t count_chunk_pair(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
+                                                     const ChunkMask& m, uint64_t iv0, uint32_t carry,
+                                                     uint32_t* gcounts, uint32_t& lane_total, uint32_t (&pin)[9],
+                                                     uint32_t (&pout)[9]) {
+    constexpr int K = 7;
+    constexpr uint32_t TM = (1u << (2 * (K - 1))) - 1u;
+    if constexpr (!MASKED) {
+        uint32_t Cf, NNL, bad;
+        classify16_fast(d, Cf, NNL, bad);
+        const uint32_t nef = (uint32_t)__builtin_popcount(NNL);
+        const bool self_ok = bad == 0 && nef >= 15u;
+        if (t_n(carry) >= (uint32_t)(K - 1) && __builtin_amdgcn_ballot_w64(!self_ok) == 0) {
+            const uint32_t r = (uint32_t)__builtin_ctz((NNL ^ 0xFFFFu) | 0x10000u);
+            const uint32_t lo1 = (1u << r) - 1u, lo2 = lo1 | (lo1 << r);
+            const uint32_t C = bfi(lo2, Cf, Cf >> 2);
+            const uint32_t pC = wave_shr1(t_codes(carry), C);
+            // X = W << 2, W = (pC : C) over nef entries (as count_chunk).  Pair j =
+            // windows 2j (newer) and 2j+1 = the 8-mer at bits [4j, 4j+16) of W: LDS
+            // word bits [4j+1, 4j+16) of W, i.e. bits [4j+3, 4j+18) of X, times 4;
+            // half = bit 4j of W.
+            const uint32_t xlo = C << 2, xhi = (pC << ((2u * nef + 2u) & 31u)) | (C >> 30);
+            const uint32_t wl = __builtin_amdgcn_alignbit(xhi, xlo, 2);   // W's low word
+            const uint32_t H0 = (wl << 4) & 0x10101010u, H1 = wl & 0x10101010u;
+            const uint32_t one = 1u;
+            const bool has7 = nef == 16u;
+            uint32_t (&rt)[9] = pout;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const uint32_t i = s_fold(fwd(r), rcw(r));
-        o |= lds_add_rtn(s_addr(i), ((R >> r) & 1u) * half_one(i));
-    }
+            for (int j = 0; j < 8; ++j) {
+                uint32_t dl;
+                switch (j) {
+                case 0: dl = shl1_byte<0>(H0, one); break;
+                case 1: dl = shl1_byte<0>(H1, one); break;
+                case 2: dl = shl1_byte<1>(H0, one); break;
+                case 3: dl = shl1_byte<1>(H1, one); break;
+                case 4: dl = shl1_byte<2>(H0, one); break;
+                case 5: dl = shl1_byte<2>(H1, one); break;
+                case 6: dl = shl1_byte<3>(H0, one); break;
+                default: dl = has7 ? shl1_byte<3>(H1, one) : 0u; break;
+                }
+                const uint32_t a = (j == 0 ? (wl << 1) : __builtin_amdgcn_alignbit(xhi, xlo, 4 * j + 1)) & kPairPMask;
+#if KF_PAIR_ABL == 1   // profiling only: no returns, no overflow check (wrong on low complexity)
+                lds_add(a, dl);
+                rt[j] = 0;
+#elif KF_PAIR_ABL == 2   // profiling only: no pair adds at all
+                lane_total += a ^ dl;
+                rt[j] = 0;
+#else
+                rt[j] = lds_add_rtn(a, dl);
+#endif
+            }
+            rt[8] = 0;
+            if (!has7) {   // window 14 (bits [28, 42) of W) alone
+                const uint32_t y = __builtin_amdgcn_alignbit(xhi, xlo, 30) & 0x3FFFu;
+                const uint32_t i = s_fold(y, kf_revcomp<K>(y));
+                rt[8] = lds_add_rtn(s_addr(i), half_one(i));
+            }
+            lane_total += nef;
+            uint32_t po = 0;
 #pragma unroll
-    for (int j = 0; j < 9; ++j) {
-        o |= pend[j];
-        pend[j] = 0;
+            for (int j = 0; j < 9; ++j) po |= pin[j];
+            if (__builtin_amdgcn_ballot_w64((po & kU16Hot) != 0) != 0) pair_scan_drain(A.code2col, gcounts, lane);
+            const uint32_t c63 = (uint32_t)__builtin_amdgcn_readlane((int)C, kWave - 1);
+            return tail_pack(c63 & TM, 31u, 31u);
+        }
     }
-    if (__builtin_amdgcn_ballot_w64((o & kU16Hot) != 0) != 0) pair_scan_drain(A.code2col, gcounts, lane);
-    lane_total += (uint32_t)__builtin_popcount(R);
+    uint32_t C, V, EN, ne, own;
+    front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
+    const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
+    pair_singles(win, A, gcounts, lane, lane_total, pin);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) pout[j] = 0;
+    return win.next;
 }
 
 // Process the wave range [lo, hi) of genome [glo, ghi).
-template <int K, bool GLOBAL, int ABL, int RING>
+template <int K, bool GLOBAL, int ABL, int RING, bool PAIR = false>
 __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                   uint64_t lo, uint64_t hi, int lane,
                                                   uint32_t* __restrict__ hist, uint32_t pass) {
     if (lo >= hi) return 0;
-    uint32_t* gcounts = GLOBAL ? A.counts + (uint64_t)g * A.nbins : nullptr;
+    uint32_t* gcounts = (GLOBAL || PAIR) ? A.counts + (uint64_t)g * A.nbins : nullptr;
+    // PAIR: returns of the last fast chunk, in set (ring slot parity)
+    uint32_t pend0[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, pend1[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_begin = A.prof ? __builtin_amdgcn_s_memtime() : 0;
     Range rg;
     rg.init(glo, ghi, lo, hi);
@@ -534,10 +654,18 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
     uint32_t rel = 0;
     const ChunkMask m = rg.mask();
     uint32_t lane_total = 0;
-    auto count = [&](const uint4 bf) {
+    auto count = [&](const uint4 bf, int slot) {
         const uint64_t cc = rg.c0 + rel;
         const bool msk = rg.masked(A, rel);
-        if (ABL == 3) {          // profiling only: stream the bytes, no counting
+        if constexpr (PAIR) {
+            static_assert(RING % 2 == 0, "pair sets alternate by ring slot");
+            uint32_t(&pin)[9] = (slot & 1) ? pend0 : pend1;
+            uint32_t(&pout)[9] = (slot & 1) ? pend1 : pend0;
+            if (msk)
+                carry = count_chunk_pair<true>(bf, A, cc, lane, m, rg.iv, carry, gcounts, lane_total, pin, pout);
+            else
+                carry = count_chunk_pair<false>(bf, A, cc, lane, m, rg.iv, carry, gcounts, lane_total, pin, pout);
+        } else if (ABL == 3) {   // profiling only: stream the bytes, no counting
             lane_total += bf.x ^ bf.y ^ bf.z ^ bf.w;
         } else if (msk)
             carry = count_chunk<K, true, GLOBAL, ABL>(bf, A, cc, lane, m, rg.iv, carry, hist, gcounts, lane_total, pass);
@@ -551,14 +679,14 @@ __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g,
     for (uint32_t i = 0; i + RING <= nch; i += RING) {
 #pragma unroll
         for (int j = 0; j < RING; ++j) {
-            count(buf[j]);
+            count(buf[j], j);
             buf[j] = rg.load(A.bytes, rel + (RING - 1) * kChunk, lane);
         }
     }
     const uint32_t rem = nch % RING;
 #pragma unroll
     for (int j = 0; j < RING - 1; ++j)
-        if (rem > (uint32_t)j) count(buf[j]);
+        if (rem > (uint32_t)j) count(buf[j], j);
     if (A.prof && lane == 0) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         const uint64_t t_end = __builtin_amdgcn_s_memtime();
@@ -581,13 +709,16 @@ __global__ void __launch_bounds__(Shape<V>::block)
     constexpr int kWaves = kBlock / kWave;
     constexpr bool GLOBAL = ModeOf<K>::mode == kModeGlobal;
     constexpr bool MULTI = ModeOf<K>::mode == kModeMulti;
-    // dynamic LDS: the histogram at offset 0 (so bin addresses need no base add),
-    // then kWaves u64 reduction slots; no static __shared__ (it would precede it)
+    constexpr bool PAIR = kStaticPair<V>;
+    static_assert(!PAIR || (K == 7 && kBlock == 1024), "static pair counting is k = 7, 1024 threads");
+    // dynamic LDS: the histogram (PAIR: P and S) at offset 0 (so bin addresses need
+    // no base add), then kWaves u64 reduction slots; no static __shared__ (it would
+    // precede it)
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    constexpr uint32_t NCODES = GLOBAL ? 4u : ModeOf<K>::lds_codes;
+    constexpr uint32_t NCODES = PAIR ? kPairCtl / 4 : (GLOBAL ? 4u : ModeOf<K>::lds_codes);
     if (!GLOBAL) {
         for (uint32_t i = tid; i < NCODES; i += kBlock) hist[i] = 0;
         __syncthreads();
@@ -622,7 +753,28 @@ __global__ void __launch_bounds__(Shape<V>::block)
         }
         unsigned long long s = 0;
         uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
-        for (uint32_t pass = 0; pass < (uint32_t)ModeOf<K>::passes; ++pass) {
+        if constexpr (PAIR) {
+            s = process_range<K, false, 0, Shape<V>::ring, true>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
+            __syncthreads();   // every add of this piece is done
+            uint32_t F[16];
+            pair_f_sums(hist, tid, F);
+            __syncthreads();   // P read
+#pragma unroll
+            for (int i = 0; i < 8; ++i) *(uint2*)(hist + i * 2048 + 2 * tid) = make_uint2(F[2 * i], F[2 * i + 1]);
+            __syncthreads();   // F in LDS words [0, 16384)
+            const uint16_t* S = (const uint16_t*)((const uint8_t*)hist + kPairSBase);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t col = tid + c * kBlock;
+                const uint32_t y = A.col2rep[col], rc = kf_revcomp<K>(y);
+                const uint32_t v = hist[y] + hist[rc] + S[s_fold(y, rc)];
+                if (v) __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();   // columns read
+            uint4* h4 = (uint4*)hist;
+            for (uint32_t i = tid; i < kPairCtl / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        for (uint32_t pass = 0; pass < (PAIR ? 0u : (uint32_t)ModeOf<K>::passes); ++pass) {
             const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl, Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane, hist, pass);
             if (Shape<V>::abl) asm volatile("" ::"v"((uint32_t)lt));   // keep ablated work alive
             const uint64_t t_f0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -702,7 +854,6 @@ __global__ void __launch_bounds__(Shape<V>::block)
 // * flush: every 8-mer counter is read once, with lane-consecutive addresses,
 //   into per-7-mer sums F (y as the older window + y as the newer window), which
 //   go back to LDS; a column then needs F[rep] + F[rc rep] + S.
-__device__ __forceinline__ uint32_t u16sum2(uint32_t w) { return (w & 0xFFFFu) + (w >> 16); }
 
 // Next genome piece of this workgroup at or after genome g (g = n: none).
 __device__ __forceinline__ int32_t pair_next_piece(const CountArgs& A, int32_t g, uint64_t span_lo, uint64_t span_hi,
@@ -823,18 +974,7 @@ __global__ void __launch_bounds__(Shape<V>::block) __attribute__((amdgpu_waves_p
         // flush (1): per forward 7-mer y, F(y) = sum_a P[4y + a] + sum_a P[a 4^7 + y];
         // thread t owns y = 2048 i + 2t + {0, 1}, i = 0..7 (lane-consecutive reads)
         uint32_t F[16];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint4 w = h4[(i * 1024 + tid) & (kPairSBase / 16 - 1)];   // words 2y .. 2y+3 of y = 2048 i + 2 tid
-            F[2 * i] = u16sum2(w.x) + u16sum2(w.y);
-            F[2 * i + 1] = u16sum2(w.z) + u16sum2(w.w);
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                const uint32_t v = hist[(a * 8192 + i * 1024 + tid) & (kPairSBase / 4 - 1)];   // halves a 4^7 + y, a 4^7 + y + 1
-                F[2 * i] += v & 0xFFFFu;
-                F[2 * i + 1] += v >> 16;
-            }
-        }
+        pair_f_sums(hist, tid, F);
         __syncthreads();   // (B) P read
 #pragma unroll
         for (int i = 0; i < 8; ++i) *(uint2*)(hist + i * 2048 + 2 * tid) = make_uint2(F[2 * i], F[2 * i + 1]);
@@ -932,9 +1072,14 @@ __device__ __forceinline__ void count_chunk_fwd(const uint4 d, const CountArgs& 
             auto addr = [&](int w) -> uint32_t { return (w < 8 ? xv[w] : (xv[w - 8] >> 16)) & M4; };
             if (lane != 0) {
                 const uint32_t inc15 = nef >> 4;   // window 15 exists iff no newline
+#ifdef KF_K1_NOADD   // profiling only (tools/build_abl.sh): the fast path without its LDS adds
+#pragma unroll
+                for (int w = 0; w < 16; ++w) lane_total += addr(w);
+#else
 #pragma unroll
                 for (int w = 0; w < 15; ++w) lds_add(addr(w), 1u);
                 lds_add(addr(15), inc15);
+#endif
                 lane_total += 15u + inc15;
             }
             return;
@@ -1207,7 +1352,10 @@ void* count_kernel_v(int k) {
 // Variants >= kFirstPairVariant are the pair kernel at k = 7 and variant 1 elsewhere.
 bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant && v <= 7; }
 bool is_dyn(int k, int v) { return k <= kLdsMaxK && (v == 8 || v == 9); }
-int effective_variant(int k, int v) { return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v)) ? 1 : v; }
+bool is_static_pair(int k, int v) { return k == 7 && (v == 10 || v == 11); }
+int effective_variant(int k, int v) {
+    return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v) && !is_static_pair(k, v)) ? 1 : v;
+}
 
 template <int V>
 void* dyn_kernel_v(int k) {
@@ -1229,6 +1377,7 @@ void* count_kernel_for(int k, int v) {
         return (void*)&pair_kernel<5>;
     }
     if (is_dyn(k, v)) return v == 9 ? dyn_kernel_v<9>(k) : dyn_kernel_v<8>(k);
+    if (is_static_pair(k, v)) return v == 11 ? (void*)&count_kernel<7, 11> : (void*)&count_kernel<7, 10>;
     v = effective_variant(k, v);
 #ifdef KF_ABLATION
     if (v == 3) return count_kernel_v<3>(k);
@@ -1261,6 +1410,7 @@ int current_variant() {
 // kernel: P + S, nothing else
 int lds_bytes_for(int k, int v) {
     if (is_pair(k, v)) return (int)kPairLdsBytes;
+    if (is_static_pair(k, v)) return (int)kPairCtl + 16 * 8;
     if (is_dyn(k, v)) return (int)(sizeof(uint32_t) << (2 * k)) + 16;
     if (k <= kLdsMaxK) return (int)(sizeof(uint32_t) << (2 * k)) + 16 * 8;
     if (k <= kMultiMaxK) return (int)(sizeof(uint32_t) << kMultiBits) + 16 * 8;
@@ -1291,9 +1441,9 @@ int launch_info(int k, int* grid, int* block, int* lds, int* variant) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return kf_fail(KF_EHIP, "hipDeviceGetAttribute(MultiprocessorCount) failed");
         if (per_cu < 1) per_cu = 1;
-        // measurement knob: at most N workgroups per CU (dynamic-chunk kernels)
+        // measurement knob: at most N workgroups per CU
         const char* e = getenv("KF_WGS_PER_CU");
-        if (e && atoi(e) >= 1 && atoi(e) < per_cu && is_dyn(k, v)) per_cu = atoi(e);
+        if (e && atoi(e) >= 1 && atoi(e) < per_cu) per_cu = atoi(e);
         gr = per_cu * cus;
     }
     *grid = gr;

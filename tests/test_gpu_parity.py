@@ -334,12 +334,14 @@ def test_arbitrary_byte_values(torch_dev, oracle, k):
     check_against_oracle(oracle, blobs, k, counts, totals, fmt=1, tag="bytes")
 
 
-def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch):
-    """k=7 pair kernel: its u16 LDS counters overflow on low-complexity sequence
-    unless the drain path moves counts out exactly (poly-A, dinucleotide and
-    satellite repeats, N-broken poly-A that fills the unpaired-window table, and
-    FASTA lines of 1-7 bases that keep every chunk on the irregular path)."""
-    monkeypatch.setenv("KF_COUNT_VARIANT", "5")
+@pytest.mark.parametrize("variant", [5, 10])
+def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, variant):
+    """k=7 pair kernels (5: self-contained chunks, 10: static wave ranges): their
+    u16 LDS counters overflow on low-complexity sequence unless the drain path
+    moves counts out exactly (poly-A, dinucleotide and satellite repeats, N-broken
+    poly-A that fills the unpaired-window table, and FASTA lines of 1-7 bases that
+    keep every chunk on the irregular path)."""
+    monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
     rng = np.random.default_rng(4242)
     sat = gen.random_seq(rng, 171).tobytes()
     polya = b"A" * 40_000_000
@@ -360,10 +362,11 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch):
     check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16-many")
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7])
+@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11])
 def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
-    """k=7 pair kernel (KF_COUNT_VARIANT 5, 6, 7: prefetch ring 6 / 4 / 8) on ragged
-    FASTA, like the default forward-histogram kernel."""
+    """k=7 pair kernels (KF_COUNT_VARIANT 5, 6, 7: self-contained chunks, prefetch
+    ring 6 / 4 / 8; 10, 11: static wave ranges, ring 6 / 8) on ragged FASTA, like
+    the default forward-histogram kernel."""
     monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
     rng = np.random.default_rng(500 + variant)
     blobs = [gen.random_fasta(rng, int(rng.integers(0, 300000)), max_records=5, n_rate=0.002, lower=0.05,
