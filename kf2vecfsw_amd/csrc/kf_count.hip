@@ -232,6 +232,9 @@ constexpr uint32_t kU16Hot = 0xC000C000u;                    // a half >= 0x4000
 // (address masks: no-ops for the real layout, keep the ablation inside its LDS)
 constexpr uint32_t kPairPMask = kPairSBase - 4u;
 constexpr uint32_t kPairSMask = kPairCtl - kPairSBase - 4u;
+// K1s (count_chunk_pair): its singles by forward 7-mer, 16384 u16 after P (32 KiB),
+// so P + S fill the 160 KiB of a CU and a single costs no revcomp/fold
+constexpr uint32_t kFwdSEnd = kPairSBase + (1u << 15);
 
 __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
     return __hip_atomic_fetch_add((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -249,6 +252,7 @@ __device__ __forceinline__ uint32_t half_one(uint32_t i) { return 1u << ((i & 1u
 
 // Rare path: move 0x4000 out of each half of the LDS word at byte address a that
 // has reached it, into the count row (compare-and-swap: each move happens once).
+template <bool FWD_S = false>   // S indexed by forward 7-mer (K1s) instead of s_fold
 __device__ __noinline__ void pair_drain(uint32_t a, const uint32_t* __restrict__ code2col, uint32_t* gcounts) {
     lds_u32* p = (lds_u32*)(uintptr_t)a;
     uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -263,7 +267,7 @@ __device__ __noinline__ void pair_drain(uint32_t a, const uint32_t* __restrict__
                 if (!((sub >> (16 * h)) & 0x4000u)) continue;
                 const uint32_t bin = 2 * w + h;   // 8-mer (P) or S slot
                 if (single) {
-                    atomicAdd(gcounts + code2col[s_unfold(bin)], 0x4000u);
+                    atomicAdd(gcounts + code2col[FWD_S ? bin : s_unfold(bin)], 0x4000u);
                 } else {
                     atomicAdd(gcounts + code2col[bin >> 2], 0x4000u);
                     atomicAdd(gcounts + code2col[bin & 0x3FFFu], 0x4000u);
@@ -380,11 +384,12 @@ struct IvCursor {
 };
 
 // Rare path: drain every hot word of P and S (one wave, CAS-exact as pair_drain).
+template <bool FWD_S = false>
 __device__ __noinline__ void pair_scan_drain(const uint32_t* __restrict__ code2col, uint32_t* gcounts, int lane) {
-    for (uint32_t w = (uint32_t)lane; w < kPairCtl / 4; w += kWave) {
+    for (uint32_t w = (uint32_t)lane; w < (FWD_S ? kFwdSEnd : kPairCtl) / 4; w += kWave) {
         const uint32_t v = __hip_atomic_load((lds_u32*)(uintptr_t)(4 * w), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (v & kU16Hot) pair_drain(4 * w, code2col, gcounts);
+        if (v & kU16Hot) pair_drain<FWD_S>(4 * w, code2col, gcounts);
     }
 }
 
@@ -547,7 +552,8 @@ __device__ __forceinline__ void count_chunk_ind(const uint4 d, const CountArgs& 
 // continues its wave's stream (lane 0's context is the carry), so every lane of
 // the fast case holds 16 windows (8 pairs) or, with a newline in its block, 15
 // (7 pairs and its oldest window as a single).  Irregular chunks go to S whole.
-// Returns are checked one chunk late as in count_chunk_ind: this chunk's land in
+// Here S is indexed by the forward 7-mer (16384 u16 after P, kFwdSEnd): a single
+// costs no revcomp/fold, and the flush adds S[y] into F(y).  Returns are checked one chunk late as in count_chunk_ind: this chunk's land in
 // pout, the previous chunk's are checked from pin.  The caller alternates two
 // register sets by ring-slot parity, so no returned word is ever copied (a copy
 // would wait for the returns before this chunk's adds go out).
@@ -603,16 +609,15 @@ __device__ __forceinline__ uint32_t count_chunk_pair(const uint4 d, const CountA
 #endif
             }
             rt[8] = 0;
-            if (!has7) {   // window 14 (bits [28, 42) of W) alone
+            if (!has7) {   // window 14 (bits [28, 42) of W) alone, by forward code
                 const uint32_t y = __builtin_amdgcn_alignbit(xhi, xlo, 30) & 0x3FFFu;
-                const uint32_t i = s_fold(y, kf_revcomp<K>(y));
-                rt[8] = lds_add_rtn(s_addr(i), half_one(i));
+                rt[8] = lds_add_rtn(kPairSBase + ((y >> 1) << 2), half_one(y));
             }
             lane_total += nef;
             uint32_t po = 0;
 #pragma unroll
             for (int j = 0; j < 9; ++j) po |= pin[j];
-            if (__builtin_amdgcn_ballot_w64((po & kU16Hot) != 0) != 0) pair_scan_drain(A.code2col, gcounts, lane);
+            if (__builtin_amdgcn_ballot_w64((po & kU16Hot) != 0) != 0) pair_scan_drain<true>(A.code2col, gcounts, lane);
             const uint32_t c63 = (uint32_t)__builtin_amdgcn_readlane((int)C, kWave - 1);
             return tail_pack(c63 & TM, 31u, 31u);
         }
@@ -620,9 +625,24 @@ __device__ __forceinline__ uint32_t count_chunk_pair(const uint4 d, const CountA
     uint32_t C, V, EN, ne, own;
     front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
     const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
-    pair_singles(win, A, gcounts, lane, lane_total, pin);
+    // irregular chunk: every counted window as a single, by forward code
+    const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
+    const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
+                            __builtin_amdgcn_alignbit(whi, wlo, 24)};
+    uint32_t o = 0;
 #pragma unroll
-    for (int j = 0; j < 9; ++j) pout[j] = 0;
+    for (int r = 0; r < 16; ++r) {
+        const int fo = (2 * r) & ~7;
+        const uint32_t y = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, 2 * K);
+        o |= lds_add_rtn(kPairSBase + ((y >> 1) << 2), ((R >> r) & 1u) * half_one(y));
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        o |= pin[j];
+        pout[j] = 0;
+    }
+    if (__builtin_amdgcn_ballot_w64((o & kU16Hot) != 0) != 0) pair_scan_drain<true>(A.code2col, gcounts, lane);
+    lane_total += (uint32_t)__builtin_popcount(R);
     return win.next;
 }
 
@@ -718,7 +738,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    constexpr uint32_t NCODES = PAIR ? kPairCtl / 4 : (GLOBAL ? 4u : ModeOf<K>::lds_codes);
+    constexpr uint32_t NCODES = PAIR ? kFwdSEnd / 4 : (GLOBAL ? 4u : ModeOf<K>::lds_codes);
     if (!GLOBAL) {
         for (uint32_t i = tid; i < NCODES; i += kBlock) hist[i] = 0;
         __syncthreads();
@@ -758,21 +778,26 @@ __global__ void __launch_bounds__(Shape<V>::block)
             __syncthreads();   // every add of this piece is done
             uint32_t F[16];
             pair_f_sums(hist, tid, F);
-            __syncthreads();   // P read
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {   // singles of y = 2048 i + 2 tid + {0, 1}
+                const uint32_t v = hist[kPairSBase / 4 + i * 1024 + tid];
+                F[2 * i] += v & 0xFFFFu;
+                F[2 * i + 1] += v >> 16;
+            }
+            __syncthreads();   // P and S read
 #pragma unroll
             for (int i = 0; i < 8; ++i) *(uint2*)(hist + i * 2048 + 2 * tid) = make_uint2(F[2 * i], F[2 * i + 1]);
             __syncthreads();   // F in LDS words [0, 16384)
-            const uint16_t* S = (const uint16_t*)((const uint8_t*)hist + kPairSBase);
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 const uint32_t col = tid + c * kBlock;
                 const uint32_t y = A.col2rep[col], rc = kf_revcomp<K>(y);
-                const uint32_t v = hist[y] + hist[rc] + S[s_fold(y, rc)];
+                const uint32_t v = hist[y] + hist[rc];
                 if (v) __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             __syncthreads();   // columns read
             uint4* h4 = (uint4*)hist;
-            for (uint32_t i = tid; i < kPairCtl / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+            for (uint32_t i = tid; i < kFwdSEnd / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
         }
         for (uint32_t pass = 0; pass < (PAIR ? 0u : (uint32_t)ModeOf<K>::passes); ++pass) {
             const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl, Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane, hist, pass);
@@ -820,12 +845,17 @@ __global__ void __launch_bounds__(Shape<V>::block)
             }
         }
         s = wave_sum(s);
-        if (lane == 0) red[wave] = s;
-        __syncthreads();
-        if (tid == 0) {
-            unsigned long long t = 0;
-            for (int w = 0; w < kWaves; ++w) t += red[w];
-            if (t) atomicAdd(A.totals + g, t);
+        if constexpr (PAIR) {   // (no LDS left for reduction slots)
+            if (lane == 0 && s) atomicAdd(A.totals + g, s);
+            __syncthreads();    // P and S zero before the next piece's adds
+        } else {
+            if (lane == 0) red[wave] = s;
+            __syncthreads();
+            if (tid == 0) {
+                unsigned long long t = 0;
+                for (int w = 0; w < kWaves; ++w) t += red[w];
+                if (t) atomicAdd(A.totals + g, t);
+            }
         }
     }
     if (A.prof && tid == 0) {
@@ -1410,7 +1440,7 @@ int current_variant() {
 // kernel: P + S, nothing else
 int lds_bytes_for(int k, int v) {
     if (is_pair(k, v)) return (int)kPairLdsBytes;
-    if (is_static_pair(k, v)) return (int)kPairCtl + 16 * 8;
+    if (is_static_pair(k, v)) return (int)kFwdSEnd;
     if (is_dyn(k, v)) return (int)(sizeof(uint32_t) << (2 * k)) + 16;
     if (k <= kLdsMaxK) return (int)(sizeof(uint32_t) << (2 * k)) + 16 * 8;
     if (k <= kMultiMaxK) return (int)(sizeof(uint32_t) << kMultiBits) + 16 * 8;
