@@ -7,8 +7,9 @@ Workload (BASELINE.json configs[1]): per GPU 1,000 synthetic 5 Mbp genomes
 generated directly in HBM.  Genomes are sharded round-robin over ranks
 (rank r owns ids r, r+N, ...); no collective touches the data path.
 
-A step = one pass of the device counter over the rank's resident batch:
-zero the [genomes x 8192] count matrix + one `kf_count_batch` launch (k=7).
+A step = one pass of the device counter over the rank's resident batch: one
+`kf_count_batch` call (k=7) as the CLI makes it, i.e. zeroing the
+[genomes x 8192] count matrix and the count kernel.
 The default run also times k=11 (BASELINE configs[4]) on the same batch and
 reports it under "secondary"; `roofline.traffic` is the measured HBM bytes per
 launch (rocprofv3 PMC, tools/pmc_traffic.py) when profiles/ holds it.
@@ -178,23 +179,20 @@ def main() -> None:
 
     def run(k, steps, warmup):
         """`warmup` untimed + `steps` timed steps at k over the resident batch.
-        A step = zero the count matrix + one kf_count_batch launch.  Returns
+        A step = one kf_count_batch call (count-matrix memset + kernel).  Returns
         (counter, counts, totals, wall s, mean kernel ms by HIP events on the
         launch stream), both max over ranks."""
         kc = C.KmerCounter(k, dev)
         counts, totals = kc.alloc_out(n)
 
-        # k <= 8: zero outside the events so they bracket the count kernel alone;
-        # k >= 9 (bucket kernels) write every count row, so no 4 x nbins memset
-        zero_first = k <= 8
+        # the same call the CLI makes (accumulate=False): for k <= 8 it zeroes the
+        # count matrix inside kf_count_batch, so the events bracket that memset and
+        # the count kernel; the k >= 9 bucket kernels write every row themselves
 
         def step(ev=None):
-            if zero_first:
-                counts.zero_()
-                totals.zero_()
             if ev is not None:
                 ev[0].record(stream)
-            kc.count(db, counts, totals, accumulate=zero_first)
+            kc.count(db, counts, totals, accumulate=False)
             if ev is not None:
                 ev[1].record(stream)
 

@@ -150,15 +150,17 @@ def get_frequencies(args) -> None:
     writer = ThreadPoolExecutor(max_workers=1)
     reads = deque(reader.submit(pack, batches[i]) for i in range(min(depth, len(batches))))
     writes = []
+    # batches whose .kf files may still be waiting for the writer: each holds a
+    # pinned count matrix (4 x bins B per genome), so the backlog is bounded
+    behind = max(1, int(os.environ.get("KF_WRITE_BEHIND", "2")))
 
-    def write(ev, host, hb, names):
+    def write(ev, host, names):
         ev.synchronize()
         t0 = now_ms()
         c = host.numpy().view(np.uint32)
         write_kf_files(args.output_dir, names, c, args.pseudocount, args.raw_cnt, args.p)
         if trace:
             tr.append(("write", names[0] if names else "", t0, now_ms()))
-        del hb   # pinned input stays alive until the copies that read it are done
 
     evs = []
     for bi, idx in enumerate(batches):
@@ -174,6 +176,9 @@ def get_frequencies(args) -> None:
                 e[0].record(stream)
                 evs.append((bi, now_ms(), e))
             db = to_device(hb, device)
+            # the pinned input is released here: PyTorch's caching host allocator
+            # keeps the block from reuse until the H2D copy queued above has run
+            del hb
             if trace:
                 e[1].record(stream)
                 th = [now_ms()]
@@ -197,7 +202,10 @@ def get_frequencies(args) -> None:
                 print(">>> Adding pseudocounts. Sample: {}".format(files_names[i]))
             if not args.raw_cnt:                       # main.py:340-341
                 print(">>> Normalizing. Sample: {}".format(files_names[i]))
-        writes.append(writer.submit(write, ev, host, hb, [samples_names[idx[j]] for j in keep]))
+        if bi >= behind:   # backpressure: at most `behind` batches queued for the writer
+            writes[bi - behind].result()
+        writes.append(writer.submit(write, ev, host, [samples_names[idx[j]] for j in keep]))
+        del host, rows, counts, db
         if trace:
             th.append(now_ms())
             tr.append(("issue", bi, th))   # after: to_device, count, pinned alloc, D2H, prints+submit
@@ -241,8 +249,12 @@ def kmers_matrix(counts: np.ndarray, k: int) -> np.ndarray:
     """float32 [n_present, k+1]: digits of each present canonical k-mer + count /
     total (main.py:165-172).  Rows in vocab (sorted canonical) order; the
     reference's rows follow Jellyfish's hash order, which its FSW consumer
-    (models.py:60-64) does not depend on.  With < 2^24 k-mers the float32 sum
-    is exact in any order, so the weights equal the reference's bit for bit."""
+    (models.py:60-64) does not depend on.  While the TOTAL k-mer count (the
+    float32 sum) stays below 2^24, that sum is exact in any order, so the
+    weights equal the reference's bit for bit.  Above 2^24 total k-mers (genomes
+    over ~17 Mbp) np.sum's pairwise float32 result depends on row order, and the
+    reference's own result then depends on Jellyfish's hash order: parity there
+    is unpinned (no fixture covers it)."""
     counts = np.asarray(counts)
     nz = np.nonzero(counts)[0]
     if nz.size == 0:
@@ -399,7 +411,7 @@ def build_parser() -> argparse.ArgumentParser:
                     help="Computes k-mer counts with 0.5 pseudocount added to each frequency value")
     pf.add_argument("-raw_cnt", action="store_true", help="Computes raw k-mer counts without normalization")
     pf.add_argument("-batch_gb", type=float, default=None,
-                    help="Input bytes per device batch (GiB). Default: about 1/4 of the input, 32 MiB..4 GiB")
+                    help="Input bytes per device batch (GiB). Default: about 1/8 of the input, 16 MiB..4 GiB")
     pf.add_argument("-device", default=None, help="torch device (default: cuda)")
     pf.set_defaults(func=get_frequencies)
 

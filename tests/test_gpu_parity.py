@@ -199,6 +199,31 @@ def test_cli_end_to_end_toy(torch_dev, toy, tmp_path):
     assert sorted(os.listdir(out)) == sorted(t[1] + ".kf" for t in toy)
 
 
+@pytest.mark.parametrize("k", [7, 11])
+def test_cli_many_batches_bounded_writer(torch_dev, oracle, tmp_path, monkeypatch, k):
+    """`get_frequencies` with far more batches than the read-ahead and write-behind
+    depths (one genome per batch): every `.kf` still equals the oracle's line, so the
+    writer backpressure and the early release of the pinned input lose nothing."""
+    from kf2vecfsw_amd import main as M
+    monkeypatch.setenv("KF_READ_AHEAD", "2")
+    monkeypatch.setenv("KF_WRITE_BEHIND", "1")
+    rng = np.random.default_rng(500 + k)
+    inp, out = tmp_path / "in", tmp_path / "out"
+    inp.mkdir()
+    out.mkdir()
+    blobs = {}
+    for i in range(9):
+        b = gen.random_fasta(rng, int(rng.integers(20000, 60000)), max_records=3, n_rate=0.001)
+        blobs[f"g{i}"] = b
+        (inp / f"g{i}.fna").write_bytes(b)
+    # -batch_gb below one file: every genome is its own batch (9 batches)
+    M.main(["get_frequencies", "-input_dir", str(inp), "-output_dir", str(out), "-k", str(k), "-p", "2",
+            "-batch_gb", "0.00001", "-raw_cnt"])
+    for name, b in blobs.items():
+        c, _ = oracle.count(b, k)
+        assert (out / f"{name}.kf").read_bytes() == oracle.kf_line(name, c, raw_cnt=True).encode(), name
+
+
 def test_genome_end_at_every_alignment(torch_dev, oracle):
     """Unterminated genomes ending at every byte offset mod 16, packed with no gap:
     the last bases sit in a vector load that straddles the genome end."""
