@@ -46,8 +46,11 @@ namespace kf {
 //   variants 10, 11: k = 7 pair counting on count_kernel's static wave ranges
 //             (count_chunk_pair), one 1024-thread workgroup per CU, ring 6 / 8;
 //             for every other k they run as variant 1
-constexpr int kNumVariants = 12;
-constexpr int kDefaultVariant = 1;
+//   variants 12, 13: k = 7 pair counting with 32-byte lanes (K1w, wide_fast),
+//             static wave ranges, one 1024-thread workgroup per CU, ring of
+//             2 / 3 iterations of 2 KiB; for every other k they run as variant 1
+constexpr int kNumVariants = 14;
+constexpr int kDefaultVariant = 13;   // K1w at k = 7; variant 1 (K1) for every other k
 constexpr int kFirstPairVariant = 5;
 #ifndef KF_PAIR_ABL
 #define KF_PAIR_ABL 0
@@ -65,7 +68,10 @@ template <> struct Shape<8> { static constexpr int block = 1024, wpe = 8, abl = 
 template <> struct Shape<9> { static constexpr int block = 1024, wpe = 8, abl = 0, ring = 6; };
 template <> struct Shape<10> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 6; };
 template <> struct Shape<11> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 8; };
-template <int V> constexpr bool kStaticPair = V == 10 || V == 11;
+template <> struct Shape<12> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // ring in 2 KiB
+template <> struct Shape<13> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 3; };
+template <int V> constexpr bool kWide = V == 12 || V == 13;
+template <int V> constexpr bool kStaticPair = V == 10 || V == 11 || kWide<V>;
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
 template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 1, ring = 4; };   // no LDS adds
@@ -646,6 +652,242 @@ __device__ __forceinline__ uint32_t count_chunk_pair(const uint4 d, const CountA
     return win.next;
 }
 
+// ---------------------------------------------------------------- K1w: wide-lane pairs
+// K1s with 32 bytes per lane: a wave iteration covers 2 KiB, lane L owning bytes
+// [32L, 32L+32) (two dwordx4 loads).  The per-lane work that does not scale with
+// the bytes -- newline removal, the context from lane L-1, the carry test, the
+// return check, the chunk bookkeeping -- is paid once per 32 bytes instead of once
+// per 16.  With at most one newline in a lane's 32 bytes (any FASTA of >= 32
+// columns) a lane holds 32 windows (16 pairs into P) or 31 (15 pairs + window 30
+// as a single into S); P and S are K1s's (forward 8-mer u16 halves, forward
+// 7-mer u16 singles), so is the flush.
+// u16 exactness: every add returns the old word and a wave checks its returns at
+// the end of the same iteration; a half seen at >= 0x4000 is drained (the whole
+// table is scanned, CAS-exact).  After a half crosses 0x4000 every wave that adds
+// to it adds at most one more iteration (<= 1024 adds to one half) before its own
+// drain, so a half stays below 0x4000 + 16 x 1024 = 0x8000.
+constexpr int kWChunk = 2 * kChunk;
+constexpr uint32_t kWideHot = 0xC000C000u;    // a half >= 0x4000
+constexpr uint32_t kWideStep = 0x4000u;
+
+// Move kWideStep out of each hot half of the LDS word at byte address a into the
+// count row until both halves are below 0x2000 (compare-and-swap: exact under
+// concurrent adds).  P word: 8-mers 2w, 2w+1; S word (a >= kPairSBase): forward
+// 7-mers 2w, 2w+1.
+__device__ __noinline__ void wide_drain(uint32_t a, const uint32_t* __restrict__ code2col, uint32_t* gcounts) {
+    lds_u32* p = (lds_u32*)(uintptr_t)a;
+    uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (cur & kWideHot) {
+        const uint32_t sub = ((cur & 0xC0000000u) ? (kWideStep << 16) : 0u) | ((cur & 0xC000u) ? kWideStep : 0u);
+        uint32_t seen = cur;
+        if (__hip_atomic_compare_exchange_strong(p, &seen, cur - sub, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            const bool single = a >= kPairSBase;
+            const uint32_t w = (single ? a - kPairSBase : a) >> 2;
+            for (uint32_t h = 0; h < 2; ++h) {
+                if (!((sub >> (16 * h)) & 0xFFFFu)) continue;
+                const uint32_t bin = 2 * w + h;
+                if (single) {
+                    atomicAdd(gcounts + code2col[bin], kWideStep);
+                } else {
+                    atomicAdd(gcounts + code2col[bin >> 2], kWideStep);       // older 7-mer
+                    atomicAdd(gcounts + code2col[bin & 0x3FFFu], kWideStep);  // newer 7-mer
+                }
+            }
+            cur -= sub;
+        } else {
+            cur = seen;
+        }
+    }
+}
+__device__ __noinline__ void wide_scan_drain(const uint32_t* __restrict__ code2col, uint32_t* gcounts, int lane) {
+    for (uint32_t w = (uint32_t)lane; w < kFwdSEnd / 4; w += kWave) {
+        const uint32_t v = __hip_atomic_load((lds_u32*)(uintptr_t)(4 * w), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (v & kWideHot) wide_drain(4 * w, code2col, gcounts);
+    }
+}
+
+struct WideBlock {
+    uint4 a, b;   // lane L: bytes [32L, 32L + 16) and [32L + 16, 32L + 32) of the 2 KiB chunk
+};
+// Lane blocks of the 2 KiB chunk at c0 + rel, clamped to align16(ghi) like load_chunk.
+__device__ __forceinline__ WideBlock wide_load(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r,
+                                               int lane) {
+    const uint32_t rec = end_r > rel ? min(end_r - rel, (uint32_t)kWChunk) : 0u;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c0 + rel), (short)0, (int)rec, 0x00020000);
+    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 32, 0, 0);
+    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 32 + 16, 0, 0);
+    WideBlock w;
+    w.a = make_uint4(v0[0], v0[1], v0[2], v0[3]);
+    w.b = make_uint4(v1[0], v1[1], v1[2], v1[3]);
+    return w;
+}
+
+// Fast case of a 2 KiB iteration (uniform): every lane's 32 bytes are bases
+// with at most one newline, and the carry is complete.  Returns false (nothing
+// counted) otherwise.
+__device__ __forceinline__ bool wide_fast(const WideBlock& d, const CountArgs& A, int lane, uint32_t& carry,
+                                          uint32_t* gcounts, uint32_t& lane_total) {
+    constexpr uint32_t TM = (1u << 12) - 1u;
+    uint32_t Ca, Na, ba, Cb, Nb, bb;
+    classify16_fast(d.a, Ca, Na, ba);   // bytes 0..15: entries 31..16
+    classify16_fast(d.b, Cb, Nb, bb);   // bytes 16..31: entries 15..0 (entry 0 = newest)
+    // not-newline mask, bit r = entry r; inv has one bit per newline
+    const uint32_t inv = ~((Na << 16) | Nb);
+    const uint32_t M1 = inv - 1u;       // entries below the newline (all if none)
+    const bool self_ok = (ba | bb) == 0 && (inv & M1) == 0;
+    carry = __builtin_amdgcn_readfirstlane(carry);   // wave-uniform: its tests run on the SALU
+    if (t_n(carry) < 6u || __builtin_amdgcn_ballot_w64(!self_ok) != 0) return false;
+    // 2-bit entry mask of M1 (a prefix mask per half: m | m << popcount(m))
+    const uint32_t m1l = M1 & 0xFFFFu, m1h = M1 >> 16;
+    const uint32_t Ml = m1l | (m1l << __builtin_popcount(m1l));
+    const uint32_t Mh = m1h | (m1h << __builtin_popcount(m1h));
+    // drop the newline entry: every entry above it moves down one
+    const uint32_t Cl = bfi(Ml, Cb, __builtin_amdgcn_alignbit(Ca, Cb, 2));
+    const uint32_t Ch = bfi(Mh, Ca, Ca >> 2);
+    // context: lane L-1's newest entries (lane 0: the carry), placed above this
+    // lane's nef = 31 or 32 entries: W = pC << 2 nef | (Ch : Cl)
+    const uint32_t pC = wave_shr1(t_codes(carry), Cl);
+    const uint32_t nl = 1u - (M1 >> 31);                 // 1 iff this lane has a newline
+    const uint64_t t = (uint64_t)pC << (32u - 2u * nl);
+    const uint32_t w0 = Cl, w1 = Ch | (uint32_t)t, w2 = (uint32_t)(t >> 32);
+    // pair j = windows 2j (newer) and 2j+1 = the 8-mer at bits [4j, 4j+16) of W:
+    // P word (8-mer >> 1) at byte address bits [4j+1, 4j+16) << 2 = (X >> 4j) &
+    // 0x1FFFC with X = W << 1; half = bit 4j of W
+    const uint32_t x0 = w0 << 1, x1 = __builtin_amdgcn_alignbit(w1, w0, 31), x2 = __builtin_amdgcn_alignbit(w2, w1, 31);
+    // X >> 16 views: pairs 4..7 and 12..15 then need a plain shift (a 2-cycle
+    // VOP2 op) instead of an alignbit each (VOP3, 4 cycles; profiles/r02/valu_rate.txt)
+    const uint32_t y0 = __builtin_amdgcn_alignbit(x1, x0, 16), y1 = __builtin_amdgcn_alignbit(x2, x1, 16);
+    constexpr uint32_t PM = 0x1FFFCu;
+    const uint32_t H0 = (w0 << 4) & 0x10101010u, H1 = w0 & 0x10101010u;
+    const uint32_t H2 = (w1 << 4) & 0x10101010u, H3 = w1 & 0x10101010u;
+    const uint32_t one = 1u;
+    uint32_t rt[16];   // returned words, OR-folded after every add is issued
+#pragma unroll
+    for (int j = 0; j < 15; ++j) {
+        uint32_t a;
+        if (j < 4) a = (x0 >> (4 * j)) & PM;
+        else if (j < 8) a = (y0 >> (4 * (j - 4))) & PM;
+        else if (j < 12) a = (x1 >> (4 * (j - 8))) & PM;
+        else a = (y1 >> (4 * (j - 12))) & PM;
+        uint32_t dl;
+        const int jj = j & 7;
+        const uint32_t He = j < 8 ? H0 : H2, Ho = j < 8 ? H1 : H3;
+        switch (jj) {
+        case 0: dl = shl1_byte<0>(He, one); break;
+        case 1: dl = shl1_byte<0>(Ho, one); break;
+        case 2: dl = shl1_byte<1>(He, one); break;
+        case 3: dl = shl1_byte<1>(Ho, one); break;
+        case 4: dl = shl1_byte<2>(He, one); break;
+        case 5: dl = shl1_byte<2>(Ho, one); break;
+        case 6: dl = shl1_byte<3>(He, one); break;
+        default: dl = shl1_byte<3>(Ho, one); break;
+        }
+#if KF_PAIR_ABL == 1   // profiling only: no returns (wrong on low complexity)
+        lds_add(a, dl);
+        rt[j] = 0;
+#else
+        rt[j] = lds_add_rtn(a, dl);
+#endif
+    }
+    {
+        // pair 15 (windows 30, 31) without a newline; with one, window 30 alone
+        // (bits [60, 74) of W) into S by its forward code
+        const uint32_t ap = (y1 >> 12) & PM;
+        const uint32_t dp = shl1_byte<3>(H3, one);
+        const uint32_t y = __builtin_amdgcn_alignbit(w2, w1, 28) & 0x3FFFu;
+        const uint32_t as = kPairSBase + ((y >> 1) << 2), ds = half_one(y);
+        const uint32_t sel = 0u - nl;
+        rt[15] = lds_add_rtn(bfi(sel, as, ap), bfi(sel, ds, dp));
+    }
+    lane_total += 32u - nl;
+    const uint32_t o = ((rt[0] | rt[1]) | (rt[2] | rt[3])) | ((rt[4] | rt[5]) | (rt[6] | rt[7])) |
+                       ((rt[8] | rt[9]) | (rt[10] | rt[11])) | ((rt[12] | rt[13]) | (rt[14] | rt[15]));
+    if (__builtin_amdgcn_ballot_w64((o & kWideHot) != 0) != 0) wide_scan_drain(A.code2col, gcounts, lane);
+    carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)Cl, kWave - 1) & TM, 31u, 31u);
+    return true;
+}
+
+// Irregular 1 KiB chunk (16-byte lane layout, count_chunk's general path): every
+// counted window as a single into S by its forward code; returns checked at once.
+template <bool MASKED>
+__device__ __forceinline__ uint32_t wide_singles(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
+                                                 const ChunkMask& m, uint64_t iv0, uint32_t carry, uint32_t* gcounts,
+                                                 uint32_t& lane_total) {
+    constexpr int K = 7;
+    uint32_t C, V, EN, ne, own;
+    front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
+    const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
+    const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
+    const uint32_t wv[4] = {wlo, __builtin_amdgcn_alignbit(whi, wlo, 8), __builtin_amdgcn_alignbit(whi, wlo, 16),
+                            __builtin_amdgcn_alignbit(whi, wlo, 24)};
+    uint32_t o = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int fo = (2 * r) & ~7;
+        const uint32_t y = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, 2 * K);
+        o |= lds_add_rtn(kPairSBase + ((y >> 1) << 2), ((R >> r) & 1u) * half_one(y));
+    }
+    if (__builtin_amdgcn_ballot_w64((o & kWideHot) != 0) != 0) wide_scan_drain(A.code2col, gcounts, lane);
+    lane_total += (uint32_t)__builtin_popcount(R);
+    return win.next;
+}
+
+// The wave range [lo, hi) of genome [glo, ghi) in 2 KiB iterations (K1w).
+template <int RING>
+__device__ __forceinline__ uint64_t process_range_wide(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
+                                                       uint64_t lo, uint64_t hi, int lane) {
+    if (lo >= hi) return 0;
+    uint32_t* gcounts = A.counts + (uint64_t)g * A.nbins;
+    Range rg;
+    rg.init(glo, ghi, lo, hi);
+    WideBlock buf[RING];
+#pragma unroll
+    for (int j = 0; j < RING; ++j) buf[j] = wide_load(A.bytes, rg.c0, j * kWChunk, rg.end_r, lane);
+    rg.warm<7>(A, lane);
+    uint32_t carry = rg.carry;
+    uint32_t rel = 0;
+    const ChunkMask m = rg.mask();
+    uint32_t lane_total = 0;
+    auto step = [&](const WideBlock& bf) {
+        const bool m0 = rg.masked(A, rel);
+        const uint64_t iv0 = rg.iv;   // first half's interval cursor (m1's test may advance it)
+        const bool m1 = rg.masked(A, rel + kChunk);
+        if (m0 || m1 || !wide_fast(bf, A, lane, carry, gcounts, lane_total)) {
+            // irregular: the two 1 KiB halves in 16-byte lane layout, singles into S
+            const uint4 h0 = rg.load(A.bytes, rel, lane);
+            if (m0)
+                carry = wide_singles<true>(h0, A, rg.c0 + rel, lane, m, iv0, carry, gcounts, lane_total);
+            else
+                carry = wide_singles<false>(h0, A, rg.c0 + rel, lane, m, iv0, carry, gcounts, lane_total);
+            if (rel + kChunk < rg.nch * kChunk) {
+                const uint4 h1 = rg.load(A.bytes, rel + kChunk, lane);
+                if (m1)
+                    carry = wide_singles<true>(h1, A, rg.c0 + rel + kChunk, lane, m, rg.iv, carry, gcounts,
+                                               lane_total);
+                else
+                    carry = wide_singles<false>(h1, A, rg.c0 + rel + kChunk, lane, m, rg.iv, carry, gcounts,
+                                                lane_total);
+            }
+        }
+        rel += kWChunk;
+    };
+    const uint32_t nw = (rg.nch + 1) / 2;   // 2 KiB iterations
+    for (uint32_t i = 0; i + RING <= nw; i += RING) {
+#pragma unroll
+        for (int j = 0; j < RING; ++j) {
+            step(buf[j]);
+            buf[j] = wide_load(A.bytes, rg.c0, rel + (RING - 1) * kWChunk, rg.end_r, lane);
+        }
+    }
+    const uint32_t rem = nw % RING;
+#pragma unroll
+    for (int j = 0; j < RING - 1; ++j)
+        if (rem > (uint32_t)j) step(buf[j]);
+    return lane_total;
+}
+
 // Process the wave range [lo, hi) of genome [glo, ghi).
 template <int K, bool GLOBAL, int ABL, int RING, bool PAIR = false>
 __device__ __forceinline__ uint64_t process_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
@@ -774,7 +1016,10 @@ __global__ void __launch_bounds__(Shape<V>::block)
         unsigned long long s = 0;
         uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
         if constexpr (PAIR) {
-            s = process_range<K, false, 0, Shape<V>::ring, true>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
+            if constexpr (kWide<V>)
+                s = process_range_wide<Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane);
+            else
+                s = process_range<K, false, 0, Shape<V>::ring, true>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
             __syncthreads();   // every add of this piece is done
             uint32_t F[16];
             pair_f_sums(hist, tid, F);
@@ -1382,7 +1627,7 @@ void* count_kernel_v(int k) {
 // Variants >= kFirstPairVariant are the pair kernel at k = 7 and variant 1 elsewhere.
 bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant && v <= 7; }
 bool is_dyn(int k, int v) { return k <= kLdsMaxK && (v == 8 || v == 9); }
-bool is_static_pair(int k, int v) { return k == 7 && (v == 10 || v == 11); }
+bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 13; }
 int effective_variant(int k, int v) {
     return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v) && !is_static_pair(k, v)) ? 1 : v;
 }
@@ -1407,7 +1652,14 @@ void* count_kernel_for(int k, int v) {
         return (void*)&pair_kernel<5>;
     }
     if (is_dyn(k, v)) return v == 9 ? dyn_kernel_v<9>(k) : dyn_kernel_v<8>(k);
-    if (is_static_pair(k, v)) return v == 11 ? (void*)&count_kernel<7, 11> : (void*)&count_kernel<7, 10>;
+    if (is_static_pair(k, v)) {
+        switch (v) {
+        case 11: return (void*)&count_kernel<7, 11>;
+        case 12: return (void*)&count_kernel<7, 12>;
+        case 13: return (void*)&count_kernel<7, 13>;
+        default: return (void*)&count_kernel<7, 10>;
+        }
+    }
     v = effective_variant(k, v);
 #ifdef KF_ABLATION
     if (v == 3) return count_kernel_v<3>(k);

@@ -314,11 +314,12 @@ def test_bucket_kernel_agrees_with_other_large_k_paths(torch_dev, monkeypatch, k
     assert torch.equal(out[9][0], out[13][0]) and torch.equal(out[9][1], out[13][1])
 
 
-@pytest.mark.parametrize("variant", [0, 2, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 8, 9])
 @pytest.mark.parametrize("k", [3, 5, 7, 8])
 def test_count_kernel_variants_match_oracle(torch_dev, oracle, monkeypatch, variant, k):
-    """The other shapes of the count kernel (KF_COUNT_VARIANT: 512-thread, 6-deep
-    prefetch ring, dynamic-chunk kernels with 4- and 6-deep rings) on ragged FASTA."""
+    """The other shapes of the count kernel (KF_COUNT_VARIANT: 512-thread, the
+    1024-thread forward histogram K1 that k=7 used before K1w, 6-deep prefetch ring,
+    dynamic-chunk kernels with 4- and 6-deep rings) on ragged FASTA."""
     monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
     rng = np.random.default_rng(300 + 10 * variant + k)
     blobs = [gen.random_fasta(rng, int(rng.integers(0, 200000)), max_records=5, n_rate=0.002, lower=0.05,
@@ -359,9 +360,10 @@ def test_arbitrary_byte_values(torch_dev, oracle, k):
     check_against_oracle(oracle, blobs, k, counts, totals, fmt=1, tag="bytes")
 
 
-@pytest.mark.parametrize("variant", [5, 10])
+@pytest.mark.parametrize("variant", [5, 10, 12, 13])
 def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, variant):
-    """k=7 pair kernels (5: self-contained chunks, 10: static wave ranges): their
+    """k=7 pair kernels (5: self-contained chunks, 10: static wave ranges, 12/13:
+    32-byte lanes): their
     u16 LDS counters overflow on low-complexity sequence unless the drain path
     moves counts out exactly (poly-A, dinucleotide and satellite repeats, N-broken
     poly-A that fills the unpaired-window table, and FASTA lines of 1-7 bases that
@@ -387,10 +389,11 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, 
     check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16-many")
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11])
+@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11, 12, 13])
 def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
     """k=7 pair kernels (KF_COUNT_VARIANT 5, 6, 7: self-contained chunks, prefetch
-    ring 6 / 4 / 8; 10, 11: static wave ranges, ring 6 / 8) on ragged FASTA, like
+    ring 6 / 4 / 8; 10, 11: static wave ranges, ring 6 / 8; 12, 13: 32-byte lanes,
+    ring 2 / 3) on ragged FASTA, like
     the default forward-histogram kernel."""
     monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
     rng = np.random.default_rng(500 + variant)

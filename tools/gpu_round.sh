@@ -8,7 +8,7 @@ REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 stop_if_fatal() { rc=$1; what=$2; echo "$what rc=$rc" >> "$OUT/steps.log"; case $rc in 0|1) ;; *) echo "FATAL $what rc=$rc"; exit $rc;; esac; }
 : > "$OUT/steps.log"
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 300 > "$OUT/pytest_gpu.log" 2>&1; stop_if_fatal $? pytest
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; stop_if_fatal $? pytest
   tail -3 "$OUT/pytest_gpu.log"
 fi
 timeout -k 10 300 python __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1; stop_if_fatal $? smoke

@@ -60,6 +60,7 @@
 #define OP_LSHLV(i) "v_lshlrev_b32_e32 %" #i ", %8, %" #i "\n"
 #define OP_MIXFF(i) "v_and_b32_e32 %" #i ", 0x3030303, %" #i "\nv_xor_b32_e32 %" #i ", %8, %" #i "\n"
 #define OP_MIX3F1S(i) "v_and_b32_e32 %" #i ", 0x3030303, %" #i "\nv_xor_b32_e32 %" #i ", %8, %" #i "\nv_lshrrev_b32_e32 %" #i ", 3, %" #i "\nv_perm_b32 %" #i ", %" #i ", %8, %9\n"
+#define OP_LSHL_INL(i) "v_lshlrev_b32_e32 %" #i ", 3, %" #i "\n"
 #define OP_CNDV(i) "v_cndmask_b32_e32 %" #i ", %8, %" #i ", vcc\n"
 #define OP_MIX(i) "v_and_b32_e32 %" #i ", %9, %" #i "\nv_perm_b32 %" #i ", %" #i ", %8, %9\n"
 
@@ -114,6 +115,10 @@ __device__ __forceinline__ void body(uint32_t& x0, uint32_t& x1, uint32_t& x2, u
     case 44: BODY(OP_LSHLV); break;
     case 45: BODY(OP_MIXFF); break;
     case 46: BODY(OP_MIX3F1S); break;
+    case 47: BODY(OP_AND_LIT); BODY(OP_PERM); break;
+    case 48: BODY(OP_AND_LIT); BODY(OP_AND_LIT); BODY(OP_PERM); BODY(OP_PERM); break;
+    case 49: BODY(OP_AND_LIT); BODY(OP_XOR); BODY(OP_LSHR); BODY(OP_AND_LIT); BODY(OP_PERM); BODY(OP_BITOP3); break;
+    case 50: BODY(OP_LSHL_INL); break;
     }
 }
 static const char* kNames[] = {"v_and_b32 (VOP2)", "v_lshrrev_b32", "v_add_u32", "v_perm_b32", "v_alignbit_b32",
@@ -128,8 +133,10 @@ static const char* kNames[] = {"v_and_b32 (VOP2)", "v_lshrrev_b32", "v_add_u32",
                                "v_or_b32_e32 sgpr", "and_e32 + perm (per pair)",
                                "v_dot4c_i32_i8_e32 vgpr", "v_mul_u32_u24_e32 vgpr", "v_mul_hi_u32_u24 vgpr",
                                "v_sub_u32_e32 vgpr", "v_min_u32_e32 vgpr", "v_lshlrev_b32_e32 vgpr",
-                               "and_lit + xor (per pair)", "3 fast + perm (per quad)"};
-constexpr int kOps = 47;
+                               "and_lit + xor (per pair)", "3 fast + perm (per quad)",
+                               "runs 8 and + 8 perm (per 2)", "runs 16 and + 16 perm (per 4)",
+                               "runs 32 fast + 16 cplx (per 6)", "v_lshlrev_b32_e32 inline"};
+constexpr int kOps = 51;
 constexpr int kUnroll = 8;   // BODY calls per iteration: 64 instructions
 
 template <int OP>
@@ -163,7 +170,8 @@ int main() {
                      k_valu<24>, k_valu<25>, k_valu<26>, k_valu<27>, k_valu<28>, k_valu<29>,
                      k_valu<30>, k_valu<31>, k_valu<32>, k_valu<33>, k_valu<34>, k_valu<35>,
                      k_valu<36>, k_valu<37>, k_valu<38>, k_valu<39>, k_valu<40>, k_valu<41>,
-                     k_valu<42>, k_valu<43>, k_valu<44>, k_valu<45>, k_valu<46>};
+                     k_valu<42>, k_valu<43>, k_valu<44>, k_valu<45>, k_valu<46>, k_valu<47>,
+                     k_valu<48>, k_valu<49>, k_valu<50>};
     unsigned long long* cyc;
     uint32_t* sink;
     const int max_waves = cus * 32;
