@@ -49,9 +49,11 @@ namespace kf {
 //   variants 12, 13: k = 7 pair counting with 32-byte lanes (K1w, wide_fast),
 //             static wave ranges, one 1024-thread workgroup per CU, ring of
 //             2 / 3 iterations of 2 KiB; for every other k they run as variant 1
-constexpr int kNumVariants = 14;
-constexpr int kDefaultVariant = 13;   // K1w at k = 7; variant 1 (K1) for every other k
+constexpr int kNumVariants = 20;
+constexpr int kDefaultVariant = 18;   // K1x at k = 7; variant 1 (K1) for every other k
 constexpr int kFirstPairVariant = 5;
+// K1x default shares by wave age slot (KF_WAVE_WEIGHTS overrides)
+constexpr uint32_t kWaveW0 = 13, kWaveW1 = 10, kWaveW2 = 8, kWaveW3 = 6;
 #ifndef KF_PAIR_ABL
 #define KF_PAIR_ABL 0
 #endif
@@ -70,8 +72,23 @@ template <> struct Shape<10> { static constexpr int block = 1024, wpe = 4, abl =
 template <> struct Shape<11> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 8; };
 template <> struct Shape<12> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // ring in 2 KiB
 template <> struct Shape<13> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 3; };
-template <int V> constexpr bool kWide = V == 12 || V == 13;
-template <int V> constexpr bool kStaticPair = V == 10 || V == 11 || kWide<V>;
+// K1w knobs: aux = cache policy of the byte-stream loads (2 = nt), late = returns
+// checked one iteration later (two register sets by ring-slot parity)
+template <> struct Shape<14> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 3, aux = 2, late = 0; };
+template <> struct Shape<15> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 4, aux = 0, late = 0; };
+template <> struct Shape<16> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 4, aux = 0, late = 1; };
+template <> struct Shape<17> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 4, aux = 2, late = 1; };
+template <int V> constexpr bool kWide = V >= 12 && V <= 17;
+template <int V> struct WideKnobs { static constexpr int aux = 0, late = 0; };
+template <> struct WideKnobs<14> { static constexpr int aux = Shape<14>::aux, late = Shape<14>::late; };
+template <> struct WideKnobs<15> { static constexpr int aux = Shape<15>::aux, late = Shape<15>::late; };
+template <> struct WideKnobs<16> { static constexpr int aux = Shape<16>::aux, late = Shape<16>::late; };
+template <> struct WideKnobs<17> { static constexpr int aux = Shape<17>::aux, late = Shape<17>::late; };
+// K1x: 48-byte lanes (3 KiB per wave iteration), table classification (x_fast)
+template <> struct Shape<18> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 3; };
+template <> struct Shape<19> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };
+template <int V> constexpr bool kX = V == 18 || V == 19;
+template <int V> constexpr bool kStaticPair = V == 10 || V == 11 || kWide<V> || kX<V>;
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
 template <> struct Shape<3> { static constexpr int block = 1024, wpe = 8, abl = 1, ring = 4; };   // no LDS adds
@@ -667,6 +684,13 @@ __device__ __forceinline__ uint32_t count_chunk_pair(const uint4 d, const CountA
 // to it adds at most one more iteration (<= 1024 adds to one half) before its own
 // drain, so a half stays below 0x4000 + 16 x 1024 = 0x8000.
 constexpr int kWChunk = 2 * kChunk;
+#ifndef KF_K1W_ABL
+// profiling-only builds (tools/build_abl.sh, wrong counts by design): 1 = no LDS
+// adds, 2 = adds without returns or checks, 3 = no classification (raw bits as
+// codes, every lane fast without a newline), 4 = stream only, 5 = K1x compute
+// only (the loads re-read the range's first chunks, cache-resident)
+#define KF_K1W_ABL 0
+#endif
 constexpr uint32_t kWideHot = 0xC000C000u;    // a half >= 0x4000
 constexpr uint32_t kWideStep = 0x4000u;
 
@@ -712,12 +736,13 @@ struct WideBlock {
     uint4 a, b;   // lane L: bytes [32L, 32L + 16) and [32L + 16, 32L + 32) of the 2 KiB chunk
 };
 // Lane blocks of the 2 KiB chunk at c0 + rel, clamped to align16(ghi) like load_chunk.
+template <int AUX = 0>
 __device__ __forceinline__ WideBlock wide_load(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r,
                                                int lane) {
     const uint32_t rec = end_r > rel ? min(end_r - rel, (uint32_t)kWChunk) : 0u;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c0 + rel), (short)0, (int)rec, 0x00020000);
-    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 32, 0, 0);
-    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 32 + 16, 0, 0);
+    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 32, 0, AUX);
+    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 32 + 16, 0, AUX);
     WideBlock w;
     w.a = make_uint4(v0[0], v0[1], v0[2], v0[3]);
     w.b = make_uint4(v1[0], v1[1], v1[2], v1[3]);
@@ -727,12 +752,22 @@ __device__ __forceinline__ WideBlock wide_load(const uint8_t* bytes, uint64_t c0
 // Fast case of a 2 KiB iteration (uniform): every lane's 32 bytes are bases
 // with at most one newline, and the carry is complete.  Returns false (nothing
 // counted) otherwise.
+// LATE: this iteration's returns go to pout and the previous fast iteration's
+// (pin) are checked before this iteration's adds go out, so no wave waits for
+// its own returns; a half then stays below 0x4000 + 16 x 2 x 1024 = 0xC000.
+template <bool LATE = false>
 __device__ __forceinline__ bool wide_fast(const WideBlock& d, const CountArgs& A, int lane, uint32_t& carry,
-                                          uint32_t* gcounts, uint32_t& lane_total) {
+                                          uint32_t* gcounts, uint32_t& lane_total, const uint32_t (&pin)[16],
+                                          uint32_t (&pout)[16]) {
     constexpr uint32_t TM = (1u << 12) - 1u;
     uint32_t Ca, Na, ba, Cb, Nb, bb;
+#if KF_K1W_ABL == 3
+    Ca = d.a.x ^ d.a.y ^ d.a.z ^ d.a.w, Cb = d.b.x ^ d.b.y ^ d.b.z ^ d.b.w;
+    Na = Nb = 0xFFFFu, ba = bb = 0;
+#else
     classify16_fast(d.a, Ca, Na, ba);   // bytes 0..15: entries 31..16
     classify16_fast(d.b, Cb, Nb, bb);   // bytes 16..31: entries 15..0 (entry 0 = newest)
+#endif
     // not-newline mask, bit r = entry r; inv has one bit per newline
     const uint32_t inv = ~((Na << 16) | Nb);
     const uint32_t M1 = inv - 1u;       // entries below the newline (all if none)
@@ -763,7 +798,13 @@ __device__ __forceinline__ bool wide_fast(const WideBlock& d, const CountArgs& A
     const uint32_t H0 = (w0 << 4) & 0x10101010u, H1 = w0 & 0x10101010u;
     const uint32_t H2 = (w1 << 4) & 0x10101010u, H3 = w1 & 0x10101010u;
     const uint32_t one = 1u;
-    uint32_t rt[16];   // returned words, OR-folded after every add is issued
+    if constexpr (LATE) {
+        const uint32_t po = ((pin[0] | pin[1]) | (pin[2] | pin[3])) | ((pin[4] | pin[5]) | (pin[6] | pin[7])) |
+                            ((pin[8] | pin[9]) | (pin[10] | pin[11])) | ((pin[12] | pin[13]) | (pin[14] | pin[15]));
+        if (__builtin_amdgcn_ballot_w64((po & kWideHot) != 0) != 0) wide_scan_drain(A.code2col, gcounts, lane);
+    }
+    uint32_t rtl[16];
+    uint32_t (&rt)[16] = LATE ? pout : rtl;   // returned words
 #pragma unroll
     for (int j = 0; j < 15; ++j) {
         uint32_t a;
@@ -784,8 +825,11 @@ __device__ __forceinline__ bool wide_fast(const WideBlock& d, const CountArgs& A
         case 6: dl = shl1_byte<3>(He, one); break;
         default: dl = shl1_byte<3>(Ho, one); break;
         }
-#if KF_PAIR_ABL == 1   // profiling only: no returns (wrong on low complexity)
+#if KF_PAIR_ABL == 1 || KF_K1W_ABL == 2   // profiling only: no returns (wrong on low complexity)
         lds_add(a, dl);
+        rt[j] = 0;
+#elif KF_K1W_ABL == 1
+        lane_total += a ^ dl;
         rt[j] = 0;
 #else
         rt[j] = lds_add_rtn(a, dl);
@@ -799,12 +843,22 @@ __device__ __forceinline__ bool wide_fast(const WideBlock& d, const CountArgs& A
         const uint32_t y = __builtin_amdgcn_alignbit(w2, w1, 28) & 0x3FFFu;
         const uint32_t as = kPairSBase + ((y >> 1) << 2), ds = half_one(y);
         const uint32_t sel = 0u - nl;
+#if KF_K1W_ABL == 1
+        lane_total += bfi(sel, as, ap) ^ bfi(sel, ds, dp);
+        rt[15] = 0;
+#elif KF_K1W_ABL == 2
+        lds_add(bfi(sel, as, ap), bfi(sel, ds, dp));
+        rt[15] = 0;
+#else
         rt[15] = lds_add_rtn(bfi(sel, as, ap), bfi(sel, ds, dp));
+#endif
     }
     lane_total += 32u - nl;
-    const uint32_t o = ((rt[0] | rt[1]) | (rt[2] | rt[3])) | ((rt[4] | rt[5]) | (rt[6] | rt[7])) |
-                       ((rt[8] | rt[9]) | (rt[10] | rt[11])) | ((rt[12] | rt[13]) | (rt[14] | rt[15]));
-    if (__builtin_amdgcn_ballot_w64((o & kWideHot) != 0) != 0) wide_scan_drain(A.code2col, gcounts, lane);
+    if constexpr (!LATE) {
+        const uint32_t o = ((rt[0] | rt[1]) | (rt[2] | rt[3])) | ((rt[4] | rt[5]) | (rt[6] | rt[7])) |
+                           ((rt[8] | rt[9]) | (rt[10] | rt[11])) | ((rt[12] | rt[13]) | (rt[14] | rt[15]));
+        if (__builtin_amdgcn_ballot_w64((o & kWideHot) != 0) != 0) wide_scan_drain(A.code2col, gcounts, lane);
+    }
     carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)Cl, kWave - 1) & TM, 31u, 31u);
     return true;
 }
@@ -814,7 +868,7 @@ __device__ __forceinline__ bool wide_fast(const WideBlock& d, const CountArgs& A
 template <bool MASKED>
 __device__ __forceinline__ uint32_t wide_singles(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
                                                  const ChunkMask& m, uint64_t iv0, uint32_t carry, uint32_t* gcounts,
-                                                 uint32_t& lane_total) {
+                                                 uint32_t& lane_total, uint32_t& drained) {
     constexpr int K = 7;
     uint32_t C, V, EN, ne, own;
     front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
@@ -829,46 +883,70 @@ __device__ __forceinline__ uint32_t wide_singles(const uint4 d, const CountArgs&
         const uint32_t y = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, 2 * K);
         o |= lds_add_rtn(kPairSBase + ((y >> 1) << 2), ((R >> r) & 1u) * half_one(y));
     }
-    if (__builtin_amdgcn_ballot_w64((o & kWideHot) != 0) != 0) wide_scan_drain(A.code2col, gcounts, lane);
+    if (__builtin_amdgcn_ballot_w64((o & kWideHot) != 0) != 0) {
+        wide_scan_drain(A.code2col, gcounts, lane);
+        drained = 1;
+    }
     lane_total += (uint32_t)__builtin_popcount(R);
     return win.next;
 }
 
 // The wave range [lo, hi) of genome [glo, ghi) in 2 KiB iterations (K1w).
-template <int RING>
+template <int RING, int AUX = 0, bool LATE = false>
 __device__ __forceinline__ uint64_t process_range_wide(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                        uint64_t lo, uint64_t hi, int lane) {
+    static_assert(!LATE || RING % 2 == 0, "late return sets alternate by ring slot");
     if (lo >= hi) return 0;
     uint32_t* gcounts = A.counts + (uint64_t)g * A.nbins;
     Range rg;
     rg.init(glo, ghi, lo, hi);
     WideBlock buf[RING];
 #pragma unroll
-    for (int j = 0; j < RING; ++j) buf[j] = wide_load(A.bytes, rg.c0, j * kWChunk, rg.end_r, lane);
+    for (int j = 0; j < RING; ++j) buf[j] = wide_load<AUX>(A.bytes, rg.c0, j * kWChunk, rg.end_r, lane);
     rg.warm<7>(A, lane);
     uint32_t carry = rg.carry;
     uint32_t rel = 0;
     const ChunkMask m = rg.mask();
     uint32_t lane_total = 0;
-    auto step = [&](const WideBlock& bf) {
+    uint32_t drained = 0;   // (K1w flushes with atomics whatever its drains)
+    uint32_t pend0[16], pend1[16];   // LATE: returns of the last fast iteration, by slot parity
+#pragma unroll
+    for (int j = 0; j < 16; ++j) pend0[j] = pend1[j] = 0;
+    auto step = [&](const WideBlock& bf, int slot) {
+#if KF_K1W_ABL == 4
+        lane_total += bf.a.x ^ bf.a.y ^ bf.a.z ^ bf.a.w ^ bf.b.x ^ bf.b.y ^ bf.b.z ^ bf.b.w;
+        rel += kWChunk;
+        return;
+#endif
+        uint32_t(&pin)[16] = (slot & 1) ? pend0 : pend1;
+        uint32_t(&pout)[16] = (slot & 1) ? pend1 : pend0;
         const bool m0 = rg.masked(A, rel);
         const uint64_t iv0 = rg.iv;   // first half's interval cursor (m1's test may advance it)
         const bool m1 = rg.masked(A, rel + kChunk);
-        if (m0 || m1 || !wide_fast(bf, A, lane, carry, gcounts, lane_total)) {
+        if (m0 || m1 || !wide_fast<LATE>(bf, A, lane, carry, gcounts, lane_total, pin, pout)) {
+            if constexpr (LATE) {   // the previous iteration's returns, then nothing pending
+                uint32_t po = 0;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    po |= pin[j];
+                    pout[j] = 0;
+                }
+                if (__builtin_amdgcn_ballot_w64((po & kWideHot) != 0) != 0) wide_scan_drain(A.code2col, gcounts, lane);
+            }
             // irregular: the two 1 KiB halves in 16-byte lane layout, singles into S
             const uint4 h0 = rg.load(A.bytes, rel, lane);
             if (m0)
-                carry = wide_singles<true>(h0, A, rg.c0 + rel, lane, m, iv0, carry, gcounts, lane_total);
+                carry = wide_singles<true>(h0, A, rg.c0 + rel, lane, m, iv0, carry, gcounts, lane_total, drained);
             else
-                carry = wide_singles<false>(h0, A, rg.c0 + rel, lane, m, iv0, carry, gcounts, lane_total);
+                carry = wide_singles<false>(h0, A, rg.c0 + rel, lane, m, iv0, carry, gcounts, lane_total, drained);
             if (rel + kChunk < rg.nch * kChunk) {
                 const uint4 h1 = rg.load(A.bytes, rel + kChunk, lane);
                 if (m1)
                     carry = wide_singles<true>(h1, A, rg.c0 + rel + kChunk, lane, m, rg.iv, carry, gcounts,
-                                               lane_total);
+                                               lane_total, drained);
                 else
                     carry = wide_singles<false>(h1, A, rg.c0 + rel + kChunk, lane, m, rg.iv, carry, gcounts,
-                                                lane_total);
+                                                lane_total, drained);
             }
         }
         rel += kWChunk;
@@ -877,14 +955,276 @@ __device__ __forceinline__ uint64_t process_range_wide(const CountArgs& A, int32
     for (uint32_t i = 0; i + RING <= nw; i += RING) {
 #pragma unroll
         for (int j = 0; j < RING; ++j) {
-            step(buf[j]);
-            buf[j] = wide_load(A.bytes, rg.c0, rel + (RING - 1) * kWChunk, rg.end_r, lane);
+            step(buf[j], j);
+            buf[j] = wide_load<AUX>(A.bytes, rg.c0, rel + (RING - 1) * kWChunk, rg.end_r, lane);
         }
     }
     const uint32_t rem = nw % RING;
 #pragma unroll
     for (int j = 0; j < RING - 1; ++j)
+        if (rem > (uint32_t)j) step(buf[j], j);
+    return lane_total;
+}
+
+// ---------------------------------------------------------------- K1x: 48-byte lanes
+// K1w with 48 bytes per lane: a wave iteration covers 3 KiB, lane L owning bytes
+// [48L, 48L+48) (three dwordx4 loads), so the per-lane work that does not scale
+// with the bytes (newline removal, context, carry, return check, bookkeeping) is
+// paid once per 48 bytes; FASTA of >= 48 columns still has at most one newline
+// per lane.  A lane holds 48 windows (24 pairs into P) or 47 (23 pairs + window
+// 46 as a single into S); P, S, the drains and the flush are K1w's.
+// Classification per dword x (4 bytes), no per-byte newline compare:
+//   s  = x & 7 per byte: A/a 1, C/c 3, T/t 4, G/g 7, '\n' 2 (distinct)
+//   e  = kXTab[s] (one v_perm): the lowercase base, 0x0B for '\n', and values
+//        whose low three bits differ from s elsewhere
+//   z  = bitop3(x, e, 0xDF..): bits other than 5 as x ^ e, bit 5 as x & ~e, so a
+//        base of either case gives 0 (e has bit 5 set: case ignored), '\n' gives
+//        exactly 1 ('*', which folds onto '\n', gives 0x21), and every other
+//        byte gives a value outside {0, 1}
+//   so z | ... & 0xFE.. != 0 flags a bad byte and the low bit of z is the
+//   newline flag, packed 8 bytes at a time by two chained v_dot4
+//   codes: (x & 6) = 2 x code (A0 C1 T2 G3), packed by v_dot4 with the weights
+//   of the 16-byte path (2x the packed byte; the shifts that merge four of them
+//   drop the factor).
+constexpr int kXChunk = 3 * kChunk;
+constexpr uint32_t kXTabLo = 0x630B6102u;   // e0..e3 = 0x02, 'a', 0x0B, 'c'
+constexpr uint32_t kXTabHi = 0x67000074u;   // e4..e7 = 't', 0x00, 0x00, 'g'
+
+struct XBlock {
+    uint4 q[3];   // lane L: bytes [48L + 16 i, 48L + 16 i + 16) of the 3 KiB chunk
+};
+template <int AUX = 0>
+__device__ __forceinline__ XBlock x_load(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r, int lane) {
+    const uint32_t rec = end_r > rel ? min(end_r - rel, (uint32_t)kXChunk) : 0u;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c0 + rel), (short)0, (int)rec, 0x00020000);
+    XBlock b;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 48 + 16 * i, 0, AUX);
+        b.q[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    return b;
+}
+
+// z = bits other than 5 (c = 1): x ^ e; bit 5 (c = 0): x & ~e  (one v_bitop3)
+__device__ __forceinline__ uint32_t x_zmap(uint32_t x, uint32_t e, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x38" : "=v"(r) : "v"(x), "v"(e), "v"(c));
+    return r;
+}
+
+// Fast case of a 3 KiB iteration (uniform): every lane's 48 bytes are bases with
+// at most one newline, and the carry is complete.  Returns false (nothing
+// counted) otherwise.  Returns are checked at the end of the iteration: after a
+// half crosses 0x4000 every wave adds at most one more iteration to it (<= 24 x 64
+// adds) before its own drain, so a half stays below 0x4000 + 16 x 1536 = 0xA000.
+__device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
+                                       uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
+    constexpr uint32_t TM = (1u << 12) - 1u;
+    const uint32_t w[12] = {d.q[0].x, d.q[0].y, d.q[0].z, d.q[0].w, d.q[1].x, d.q[1].y,
+                            d.q[1].z, d.q[1].w, d.q[2].x, d.q[2].y, d.q[2].z, d.q[2].w};
+    const uint32_t cdf = 0xDFDFDFDFu;
+    uint32_t pc[12], z[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        const uint32_t x = w[i];
+        const uint32_t e = __builtin_amdgcn_perm(kXTabHi, kXTabLo, x & 0x07070707u);
+        z[i] = x_zmap(x, e, cdf);
+        pc[i] = __builtin_amdgcn_udot4(x & 0x06060606u, 0x01041040u, 0u, false);   // 2 x packed codes
+    }
+    // codes: C2 = entries 32..47 (bytes 0..15), C1 = 16..31, C0 = 0..15 (entry 0 = byte 47)
+    uint32_t C[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int b = 4 * (2 - i);
+        C[i] = (pc[b] << 23) | (pc[b + 1] << 15) | (pc[b + 2] << 7) | (pc[b + 3] >> 1);
+    }
+    // newline flags (low bit of z), 8 bytes per byte of the mask: bit r = entry r
+    uint32_t g[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+        g[q] = __builtin_amdgcn_udot4(z[2 * q], 0x10204080u, __builtin_amdgcn_udot4(z[2 * q + 1], 0x01020408u, 0u, false),
+                                      false);
+    const uint32_t NL1 = __builtin_amdgcn_perm(g[0], g[1], 0x0C0C0400u);   // entries 32..47
+    const uint32_t NL0 = (__builtin_amdgcn_perm(g[2], g[3], 0x0C0C0400u) << 16) | __builtin_amdgcn_perm(g[4], g[5], 0x0C0C0400u);
+    const uint32_t bz = ((z[0] | z[1] | z[2]) | (z[3] | z[4] | z[5])) | ((z[6] | z[7] | z[8]) | (z[9] | z[10] | z[11]));
+    const uint32_t nl = (uint32_t)__builtin_popcount(NL0) + (uint32_t)__builtin_popcount(NL1);
+    const bool self_ok = ((bz & 0xFEFEFEFEu) | (nl & ~1u)) == 0;
+    carry = __builtin_amdgcn_readfirstlane(carry);   // wave-uniform: its tests run on the SALU
+    if (t_n(carry) < 6u || __builtin_amdgcn_ballot_w64(!self_ok) != 0) return false;
+    // drop the newline entry: entries below it stay, every entry above moves down one
+    const uint64_t M = (((uint64_t)NL1 << 32) | NL0) - 1u;   // entries below the newline (all if none)
+    const uint32_t ML = (uint32_t)M, MH = (uint32_t)(M >> 32);
+    const uint32_t m0 = ML & 0xFFFFu, m1 = ML >> 16, m2 = MH & 0xFFFFu;
+    const uint32_t E0 = m0 | (m0 << __builtin_popcount(m0));
+    const uint32_t E1 = m1 | (m1 << __builtin_popcount(m1));
+    const uint32_t E2 = m2 | (m2 << __builtin_popcount(m2));
+    const uint32_t c0 = bfi(E0, C[0], __builtin_amdgcn_alignbit(C[1], C[0], 2));
+    const uint32_t c1 = bfi(E1, C[1], __builtin_amdgcn_alignbit(C[2], C[1], 2));
+    const uint32_t c2 = bfi(E2, C[2], C[2] >> 2);
+    // context: lane L-1's newest entries (lane 0: the carry) above this lane's
+    // n = 48 - nl entries: W = pC << 2n | (c2 : c1 : c0)
+    const uint32_t pC = wave_shr1(t_codes(carry), c0);
+    const uint64_t t = (uint64_t)pC << (32u - 2u * nl);
+    const uint32_t w0 = c0, w1 = c1, w2 = c2 | (uint32_t)t, w3 = (uint32_t)(t >> 32);
+    // pair j = windows 2j (newer) and 2j+1 = the 8-mer at bits [4j, 4j+16) of W:
+    // P word address = (X >> 4j) & 0x1FFFC with X = W << 1; half = bit 4j of W.
+    // Views: X dwords and X >> 16 (Y), so every pair is a plain shift and an and.
+    const uint32_t x0 = w0 << 1, x1 = __builtin_amdgcn_alignbit(w1, w0, 31), x2 = __builtin_amdgcn_alignbit(w2, w1, 31),
+                   x3 = __builtin_amdgcn_alignbit(w3, w2, 31);
+    const uint32_t X[3] = {x0, x1, x2};
+    const uint32_t Y[3] = {__builtin_amdgcn_alignbit(x1, x0, 16), __builtin_amdgcn_alignbit(x2, x1, 16),
+                           __builtin_amdgcn_alignbit(x3, x2, 16)};
+    const uint32_t Wd[3] = {w0, w1, w2};
+    constexpr uint32_t PM = 0x1FFFCu;
+    const uint32_t one = 1u;
+    uint32_t rt[24];
+#pragma unroll
+    for (int j = 0; j < 23; ++j) {
+        const int i = j >> 3, tt = j & 7;
+        const uint32_t a = ((tt < 4 ? X[i] : Y[i]) >> (4 * (tt & 3))) & PM;
+        const uint32_t H = (tt & 1) ? (Wd[i] & 0x10101010u) : ((Wd[i] << 4) & 0x10101010u);
+        uint32_t dl;
+        switch (tt >> 1) {
+        case 0: dl = shl1_byte<0>(H, one); break;
+        case 1: dl = shl1_byte<1>(H, one); break;
+        case 2: dl = shl1_byte<2>(H, one); break;
+        default: dl = shl1_byte<3>(H, one); break;
+        }
+#if KF_K1W_ABL == 2
+        lds_add(a, dl);
+        rt[j] = 0;
+#elif KF_K1W_ABL == 1
+        lane_total += a ^ dl;
+        rt[j] = 0;
+#else
+        rt[j] = lds_add_rtn(a, dl);
+#endif
+    }
+    {
+        // pair 23 (windows 46, 47) without a newline; with one, window 46 alone
+        // into S by its forward code y = bits [92, 106) of W.  Both addresses come
+        // from one view: v = X >> 92, P address v & 0x1FFFC, S address
+        // kPairSBase | (v & 0x7FFC) (= (y >> 1) << 2); both halves are bit 92 of W.
+        const uint32_t v = Y[2] >> 12;
+        const uint32_t sel = 0u - nl;
+        const uint32_t a23 = bfi(sel, kPairSBase | (v & 0x7FFCu), v & PM);
+        const uint32_t d23 = shl1_byte<3>(w2 & 0x10101010u, one);
+#if KF_K1W_ABL == 1
+        lane_total += a23 ^ d23;
+        rt[23] = 0;
+#elif KF_K1W_ABL == 2
+        lds_add(a23, d23);
+        rt[23] = 0;
+#else
+        rt[23] = lds_add_rtn(a23, d23);
+#endif
+    }
+    lane_total += 48u - nl;
+#ifdef KF_K1X_PAD   // profiling only: N extra VALU ops of one kind (1 = v_xor VOP2, 2 = v_perm VOP3)
+    {
+        uint32_t pad[4] = {w[0], w[1], w[2], w[3]};   // four independent chains
+#pragma unroll
+        for (int i = 0; i < KF_K1X_PAD_N; ++i) {
+#if KF_K1X_PAD == 1
+            asm volatile("v_xor_b32_e32 %0, %1, %0" : "+v"(pad[i & 3]) : "v"(w[i % 12]));
+#else
+            asm volatile("v_perm_b32 %0, %1, %0, %2" : "+v"(pad[i & 3]) : "v"(w[i % 12]), "v"(w[(i + 5) % 12]));
+#endif
+        }
+        lane_total += (pad[0] ^ pad[1] ^ pad[2] ^ pad[3]) & 1u;
+    }
+#endif
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < 24; j += 3) o |= rt[j] | rt[j + 1] | rt[j + 2];
+    if (__builtin_amdgcn_ballot_w64((o & kWideHot) != 0) != 0) {
+        wide_scan_drain(A.code2col, gcounts, lane);
+        drained = 1;
+    }
+    carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)c0, kWave - 1) & TM, 31u, 31u);
+    return true;
+}
+
+// The wave range [lo, hi) of genome [glo, ghi) in 3 KiB iterations (K1x).
+// `drained` is set if a u16 half of this range was moved to the count row (the
+// flush then adds with atomics).
+template <int RING>
+__device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
+                                                    uint64_t lo, uint64_t hi, int lane, uint32_t& drained) {
+    if (lo >= hi) return 0;
+    uint32_t* gcounts = A.counts + (uint64_t)g * A.nbins;
+    const uint64_t t_begin = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+    Range rg;
+    rg.init(glo, ghi, lo, hi);
+    XBlock buf[RING];
+#pragma unroll
+    for (int j = 0; j < RING; ++j) buf[j] = x_load(A.bytes, rg.c0, j * kXChunk, rg.end_r, lane);
+    rg.warm16<7>(A, lane);
+    uint64_t t_loop = 0;
+    if (A.prof) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        t_loop = __builtin_amdgcn_s_memtime();
+    }
+    uint32_t carry = rg.carry;
+    uint32_t rel = 0;
+    const ChunkMask m = rg.mask();
+    uint32_t lane_total = 0;
+    auto step = [&](const XBlock& bf) {
+#if KF_K1W_ABL == 4
+        lane_total += bf.q[0].x ^ bf.q[0].w ^ bf.q[1].y ^ bf.q[1].z ^ bf.q[2].x ^ bf.q[2].w;
+        rel += kXChunk;
+        return;
+#endif
+        // interval cursor before each 1 KiB third (a later test may advance it)
+        const bool m0 = rg.masked(A, rel);
+        const uint64_t iv0 = rg.iv;
+        const bool m1 = rg.masked(A, rel + kChunk);
+        const uint64_t iv1 = rg.iv;
+        const bool m2 = rg.masked(A, rel + 2 * kChunk);
+        if (m0 || m1 || m2 || !x_fast(bf, A, lane, carry, gcounts, lane_total, drained)) {
+            // irregular: the three 1 KiB thirds in 16-byte lane layout, singles into S
+#pragma unroll
+            for (int h = 0; h < 3; ++h) {
+                const uint32_t r = rel + h * kChunk;
+                if (h > 0 && r >= rg.nch * kChunk) break;
+                const bool mh = h == 0 ? m0 : (h == 1 ? m1 : m2);
+                const uint64_t ivh = h == 0 ? iv0 : (h == 1 ? iv1 : rg.iv);
+                const uint4 hb = rg.load(A.bytes, r, lane);
+                if (mh)
+                    carry = wide_singles<true>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
+                else
+                    carry = wide_singles<false>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
+            }
+        }
+        rel += kXChunk;
+    };
+    const uint32_t nx = (rg.nch + 2) / 3;   // 3 KiB iterations
+    for (uint32_t i = 0; i + RING <= nx; i += RING) {
+#pragma unroll
+        for (int j = 0; j < RING; ++j) {
+            step(buf[j]);
+#if KF_K1W_ABL == 5   // profiling only: every iteration re-reads the range's first chunks (cache hits)
+            buf[j] = x_load(A.bytes, rg.c0, (uint32_t)j * kXChunk, rg.end_r, lane);
+#else
+            buf[j] = x_load(A.bytes, rg.c0, rel + (RING - 1) * kXChunk, rg.end_r, lane);
+#endif
+        }
+    }
+    const uint32_t rem = nx % RING;
+#pragma unroll
+    for (int j = 0; j < RING - 1; ++j)
         if (rem > (uint32_t)j) step(buf[j]);
+    if (A.prof && lane == 0) {   // KF_COUNT_PROFILE=1: per-wave-slot loop cycles per 1 KiB chunk
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const uint64_t t_end = __builtin_amdgcn_s_memtime();
+        const int w = (int)(threadIdx.x >> 6);
+        atomicAdd(A.prof + 0, (unsigned long long)(t_loop - t_begin));
+        atomicAdd(A.prof + 1, (unsigned long long)(t_end - t_loop));
+        atomicAdd(A.prof + 2, 1ull);
+        atomicAdd(A.prof + 8 + w, (unsigned long long)(t_end - t_loop));
+        atomicAdd(A.prof + 24 + w, (unsigned long long)rg.nch);
+    }
     return lane_total;
 }
 
@@ -1006,7 +1346,14 @@ __global__ void __launch_bounds__(Shape<V>::block)
         const uint64_t plo = max(glo, span_lo), phi = min(ghi, span_hi);
         if (phi <= plo) continue;
         // wave w owns [split(w), split(w+1)): 16-byte aligned, monotone, covering [plo, phi)
-        const uint64_t lo_c = split_at(plo, phi, wave, kWaves), hi_c = split_at(plo, phi, wave + 1, kWaves);
+        uint64_t lo_c, hi_c;
+        if constexpr (kX<V>) {   // K1x: parts weighted by wave slot (KF_WAVE_WEIGHTS)
+            lo_c = split_at_w(plo, phi, (uint32_t)wave, A.wave_w);
+            hi_c = split_at_w(plo, phi, (uint32_t)wave + 1, A.wave_w);
+        } else {
+            lo_c = split_at(plo, phi, wave, kWaves);
+            hi_c = split_at(plo, phi, wave + 1, kWaves);
+        }
         if (GLOBAL) {
             const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl, Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
             const unsigned long long s = wave_sum(lt);
@@ -1016,11 +1363,22 @@ __global__ void __launch_bounds__(Shape<V>::block)
         unsigned long long s = 0;
         uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
         if constexpr (PAIR) {
-            if constexpr (kWide<V>)
-                s = process_range_wide<Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane);
+            uint32_t drained = kX<V> ? 0u : 1u;   // K1x: plain row stores unless a half was drained
+            if constexpr (kX<V>)
+                s = process_range_x<Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane, drained);
+            else if constexpr (kWide<V>)
+                s = process_range_wide<Shape<V>::ring, WideKnobs<V>::aux, WideKnobs<V>::late != 0>(
+                    A, g, glo, ghi, lo_c, hi_c, lane);
             else
                 s = process_range<K, false, 0, Shape<V>::ring, true>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
+            const uint64_t t_p0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+            // the columns' forward representatives, loaded before the barrier so
+            // their latency overlaps it
+            uint32_t rep[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) rep[c] = A.col2rep[tid + c * kBlock];
             __syncthreads();   // every add of this piece is done
+            const uint64_t t_p1 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             uint32_t F[16];
             pair_f_sums(hist, tid, F);
 #pragma unroll
@@ -1032,17 +1390,35 @@ __global__ void __launch_bounds__(Shape<V>::block)
             __syncthreads();   // P and S read
 #pragma unroll
             for (int i = 0; i < 8; ++i) *(uint2*)(hist + i * 2048 + 2 * tid) = make_uint2(F[2 * i], F[2 * i + 1]);
-            __syncthreads();   // F in LDS words [0, 16384)
+            if (lane == 0) hist[16384 + wave] = drained;   // (words past F are free now)
+            __syncthreads();   // F in LDS words [0, 16384), drain flags after it
+            // A whole genome in this span with no drained half: no other workgroup
+            // and nothing else touches row g, which the caller zeroed, so it is
+            // written with plain stores; otherwise coalesced atomics.
+            const uint4* fl = (const uint4*)(hist + 16384);
+            const uint4 f0 = fl[0], f1 = fl[1], f2 = fl[2], f3 = fl[3];
+            const bool any_drain = (f0.x | f0.y | f0.z | f0.w | f1.x | f1.y | f1.z | f1.w | f2.x | f2.y | f2.z | f2.w |
+                                    f3.x | f3.y | f3.z | f3.w) != 0;
+            const bool store = plo == glo && phi == ghi && !any_drain && !(A.flags & KF_ACCUMULATE);
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 const uint32_t col = tid + c * kBlock;
-                const uint32_t y = A.col2rep[col], rc = kf_revcomp<K>(y);
+                const uint32_t y = rep[c], rc = kf_revcomp<K>(y);
                 const uint32_t v = hist[y] + hist[rc];
-                if (v) __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (store) {
+                    if (v) gc[col] = v;
+                } else if (v) {
+                    __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
             __syncthreads();   // columns read
             uint4* h4 = (uint4*)hist;
             for (uint32_t i = tid; i < kFwdSEnd / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+            if (A.prof && tid == 0) {   // barrier wait of wave 0 and the flush, per piece
+                atomicAdd(A.prof + 3, (unsigned long long)(t_p1 - t_p0));
+                atomicAdd(A.prof + 4, 1ull);
+                atomicAdd(A.prof + 5, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_p1));
+            }
         }
         for (uint32_t pass = 0; pass < (PAIR ? 0u : (uint32_t)ModeOf<K>::passes); ++pass) {
             const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl, Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane, hist, pass);
@@ -1114,6 +1490,10 @@ __global__ void __launch_bounds__(Shape<V>::block)
         const int hb = blockIdx.x * 2 >= gridDim.x;
         atomicAdd(A.prof + 46 + hb, (unsigned long long)(rt1 - rt0));
         atomicMax(A.prof + 48 + hb, (unsigned long long)(rt1 - rt0));
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u;   // HW_REG_XCC_ID[2:0]
+        atomicAdd(A.prof + 56 + xcc, (unsigned long long)(rt1 - rt0));
+        atomicMax(A.prof + 64 + xcc, (unsigned long long)(rt1 - rt0));
+        atomicAdd(A.prof + 72 + xcc, 1ull);
     }
 }
 
@@ -1487,6 +1867,10 @@ __global__ void __launch_bounds__(Shape<V>::block) __attribute__((amdgpu_waves_p
         const int hb = blockIdx.x * 2 >= gridDim.x;
         atomicAdd(A.prof + 46 + hb, (unsigned long long)(rt1 - rt0));
         atomicMax(A.prof + 48 + hb, (unsigned long long)(rt1 - rt0));
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u;   // HW_REG_XCC_ID[2:0]
+        atomicAdd(A.prof + 56 + xcc, (unsigned long long)(rt1 - rt0));
+        atomicMax(A.prof + 64 + xcc, (unsigned long long)(rt1 - rt0));
+        atomicAdd(A.prof + 72 + xcc, 1ull);
     }
 }
 
@@ -1627,7 +2011,7 @@ void* count_kernel_v(int k) {
 // Variants >= kFirstPairVariant are the pair kernel at k = 7 and variant 1 elsewhere.
 bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant && v <= 7; }
 bool is_dyn(int k, int v) { return k <= kLdsMaxK && (v == 8 || v == 9); }
-bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 13; }
+bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 19; }
 int effective_variant(int k, int v) {
     return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v) && !is_static_pair(k, v)) ? 1 : v;
 }
@@ -1657,6 +2041,12 @@ void* count_kernel_for(int k, int v) {
         case 11: return (void*)&count_kernel<7, 11>;
         case 12: return (void*)&count_kernel<7, 12>;
         case 13: return (void*)&count_kernel<7, 13>;
+        case 14: return (void*)&count_kernel<7, 14>;
+        case 15: return (void*)&count_kernel<7, 15>;
+        case 16: return (void*)&count_kernel<7, 16>;
+        case 17: return (void*)&count_kernel<7, 17>;
+        case 18: return (void*)&count_kernel<7, 18>;
+        case 19: return (void*)&count_kernel<7, 19>;
         default: return (void*)&count_kernel<7, 10>;
         }
     }
@@ -1686,6 +2076,20 @@ int current_variant() {
     if (!e || !*e) return kDefaultVariant;
     const int v = atoi(e);
     return (v >= 0 && v < kNumVariants) ? v : kDefaultVariant;
+}
+
+// KF_WAVE_WEIGHTS="a0,a1,a2,a3" (tuning/A-B knob, read per launch), each 1..255:
+// K1x's share of a genome piece per wave of age slot 0..3 (split_at_w).
+uint32_t wave_weights() {
+    uint32_t w[4] = {kWaveW0, kWaveW1, kWaveW2, kWaveW3};
+    const char* e = getenv("KF_WAVE_WEIGHTS");
+    if (e && *e) {
+        uint32_t t[4];
+        if (sscanf(e, "%u,%u,%u,%u", &t[0], &t[1], &t[2], &t[3]) == 4 && t[0] >= 1 && t[0] <= 255 && t[1] >= 1 &&
+            t[1] <= 255 && t[2] >= 1 && t[2] <= 255 && t[3] >= 1 && t[3] <= 255)
+            for (int i = 0; i < 4; ++i) w[i] = t[i];
+    }
+    return w[0] | (w[1] << 8) | (w[2] << 16) | (w[3] << 24);
 }
 
 // histogram (4^k u32) + one u64 reduction slot per wave (16 waves max); pair
@@ -1775,9 +2179,11 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.nbins = (uint32_t)nb;
     A.n_genomes = n_genomes;
     A.prof = nullptr;
+    A.wave_w = wave_weights();
+    A.flags = flags;
     const char* pe = getenv("KF_COUNT_PROFILE");   // debugging aid: synchronous, prints to stderr
     if (pe && *pe == '1' && !bucket) {
-        if (hipMalloc((void**)&A.prof, 56 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 56 * 8, s) != hipSuccess ||
+        if (hipMalloc((void**)&A.prof, 80 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 80 * 8, s) != hipSuccess ||
             hipMemsetAsync(A.prof + 42, 0xFF, 8, s) != hipSuccess)
             return kf_fail(KF_EHIP, "profile buffer");
     }
@@ -1793,7 +2199,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (A.prof) {
-        unsigned long long h[56];
+        unsigned long long h[80];
         float ms = 0.f;
         if (hipEventRecord(pe1, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess ||
             hipEventElapsedTime(&ms, pe0, pe1) != hipSuccess ||
@@ -1814,6 +2220,10 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
                 (double)h[0] / nr, (double)h[1] / nr, h[4], (double)h[3] / nf, (double)h[5] / nf, (double)h[6] / nf);
         if (h[41])
             fprintf(stderr, "  shader clock %.3f GHz over the workgroups' lifetimes\n", (double)h[40] / (double)h[41] * 0.1);
+        for (int x = 0; x < 8; ++x)
+            if (h[72 + x])
+                fprintf(stderr, "  XCC %d: %llu workgroups, lifetime mean %.3f max %.3f ms\n", x, h[72 + x],
+                        (double)h[56 + x] / (double)h[72 + x] * 1e-5, (double)h[64 + x] * 1e-5);
         for (int w = 0; w < 16; ++w)
             if (h[24 + w])
                 fprintf(stderr, "  wave %2d: %.0f cyc/chunk over %llu chunks\n", w, (double)h[8 + w] / h[24 + w],

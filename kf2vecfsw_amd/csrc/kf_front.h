@@ -23,6 +23,8 @@ struct CountArgs {
     uint32_t nbins;
     int32_t n_genomes;
     unsigned long long* prof;      // optional cycle counters (KF_COUNT_PROFILE=1), else null
+    uint32_t wave_w;               // K1x: share of a genome piece by wave slot (4 x 8 bit, see split_at_w)
+    uint32_t flags;                // kf_count_batch flags (KF_ACCUMULATE)
 };
 
 // ---------------------------------------------------------------- tails
@@ -385,6 +387,35 @@ struct Range {
         }
         find_interval(A, lane);
     }
+    // As warm, from the 16 bytes before c0 and one interval search (the common
+    // case: they lie inside the genome, outside every excluded interval, and end
+    // in >= k-1 bases); anything else takes warm.  Same carry as warm for every
+    // use (codes of the last k-1 entries, a run of >= k-1).
+    template <int K>
+    __device__ __forceinline__ void warm16(const CountArgs& A, int lane) {
+        if (c0 < glo + 16) {   // the genome start is within reach
+            warm<K>(A, lane);
+            return;
+        }
+        const uint64_t p16 = c0 - 16;
+        const uint4 d = *(const uint4*)(A.bytes + p16);   // the same 16 bytes in every lane
+        iv = wave_upper_bound(A.n_excl, p16, lane, [&](uint64_t i) { return A.excl[2 * i + 1]; });
+        uint64_t s_iv = ~0ull, e_iv = ~0ull;
+        if (iv < A.n_excl) {
+            s_iv = uload64(A.excl + 2 * iv);
+            e_iv = uload64(A.excl + 2 * iv + 1);
+        }
+        uint32_t C, V, EN, ne, own;
+        const ChunkMask m{glo, 0, 0};
+        front_end<K, false>(d, A, p16, lane, m, iv, C, V, EN, ne, own);
+        if (s_iv < c0 || t_n(own) < (uint32_t)(K - 1)) {   // an interval ends past p16 but starts before c0
+            warm<K>(A, lane);
+            return;
+        }
+        carry = own;
+        ivs_r = iv < A.n_excl ? rel_of(s_iv) : 0xFFFFFFFFu;
+        ive_r = iv < A.n_excl ? rel_of(e_iv) : 0xFFFFFFFFu;
+    }
     // As warm, with the first chunk before c0 already loaded (ctx_load).
     template <int K>
     __device__ __forceinline__ void warm_from(const CountArgs& A, const uint4 dctx, int lane) {
@@ -435,6 +466,27 @@ __device__ __forceinline__ uint64_t split_at(uint64_t plo, uint64_t phi, uint64_
     const uint64_t len = phi - plo;
     const uint64_t s = (plo + len / n * w + (len % n) * w / n) & ~(uint64_t)15;
     return min(max(s, plo), phi);
+}
+
+// As split_at with wave w's part proportional to byte (w >> 2) of `wts` (the
+// wave's age slot on its SIMD: the SIMD issues oldest-first, so slot 0 runs
+// fastest); n = 16.  wts = 0x01010101 is an equal split.
+__device__ __forceinline__ uint64_t split_at_w(uint64_t plo, uint64_t phi, uint32_t w, uint32_t wts) {
+    if (w == 0) return plo;
+    if (w >= 16) return phi;
+    const uint32_t b0 = wts & 0xFFu, b1 = (wts >> 8) & 0xFFu, b2 = (wts >> 16) & 0xFFu, b3 = wts >> 24;
+    const uint32_t tot = 4u * (b0 + b1 + b2 + b3);
+    // prefix weight of waves 0..w-1: full slots below w's slot plus w's own slot members
+    const uint32_t s = w >> 2, r = w & 3u;
+    uint32_t cum = 0;
+    cum += (s > 0 ? 4u * b0 : (r ? r * b0 : 0u));
+    cum += (s > 1 ? 4u * b1 : (s == 1 ? r * b1 : 0u));
+    cum += (s > 2 ? 4u * b2 : (s == 2 ? r * b2 : 0u));
+    cum += (s == 3 ? r * b3 : 0u);
+    const uint64_t len = phi - plo;
+    const uint64_t q = (uint64_t)(((unsigned __int128)len * cum) / tot);
+    const uint64_t x = (plo + q) & ~(uint64_t)15;
+    return min(max(x, plo), phi);
 }
 
 // Window register of one lane's block (general path): context from lane L-1
