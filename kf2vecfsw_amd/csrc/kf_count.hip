@@ -1033,11 +1033,13 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
         pc[i] = __builtin_amdgcn_udot4(x & 0x06060606u, 0x01041040u, 0u, false);   // 2 x packed codes
     }
     // codes: C2 = entries 32..47 (bytes 0..15), C1 = 16..31, C0 = 0..15 (entry 0 = byte 47)
+    // (pc < 512 and even: pc[b] << 8 | pc[b + 1] is twice the 16-bit code of 8 bases)
     uint32_t C[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const int b = 4 * (2 - i);
-        C[i] = (pc[b] << 23) | (pc[b + 1] << 15) | (pc[b + 2] << 7) | (pc[b + 3] >> 1);
+        const uint32_t t01 = (pc[b] << 8) | pc[b + 1], t23 = (pc[b + 2] << 8) | pc[b + 3];
+        C[i] = (t01 << 15) | (t23 >> 1);
     }
     // newline flags (low bit of z), 8 bytes per byte of the mask: bit r = entry r
     uint32_t g[6];
@@ -1120,7 +1122,7 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
         rt[23] = lds_add_rtn(a23, d23);
 #endif
     }
-    lane_total += 48u - nl;
+    lane_total -= nl;   // + 48 per fast iteration, added by the caller
 #ifdef KF_K1X_PAD   // profiling only: N extra VALU ops of one kind (1 = v_xor VOP2, 2 = v_perm VOP3)
     {
         uint32_t pad[4] = {w[0], w[1], w[2], w[3]};   // four independent chains
@@ -1170,6 +1172,7 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
     uint32_t rel = 0;
     const ChunkMask m = rg.mask();
     uint32_t lane_total = 0;
+    uint32_t nfast = 0;   // fast iterations (wave-uniform): 48 windows per lane each, less its newlines
     auto step = [&](const XBlock& bf) {
 #if KF_K1W_ABL == 4
         lane_total += bf.q[0].x ^ bf.q[0].w ^ bf.q[1].y ^ bf.q[1].z ^ bf.q[2].x ^ bf.q[2].w;
@@ -1182,7 +1185,9 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         const bool m1 = rg.masked(A, rel + kChunk);
         const uint64_t iv1 = rg.iv;
         const bool m2 = rg.masked(A, rel + 2 * kChunk);
-        if (m0 || m1 || m2 || !x_fast(bf, A, lane, carry, gcounts, lane_total, drained)) {
+        const bool fast = !(m0 || m1 || m2) && x_fast(bf, A, lane, carry, gcounts, lane_total, drained);
+        nfast += fast ? 1u : 0u;
+        if (!fast) {
             // irregular: the three 1 KiB thirds in 16-byte lane layout, singles into S
 #pragma unroll
             for (int h = 0; h < 3; ++h) {
@@ -1225,7 +1230,7 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         atomicAdd(A.prof + 8 + w, (unsigned long long)(t_end - t_loop));
         atomicAdd(A.prof + 24 + w, (unsigned long long)rg.nch);
     }
-    return lane_total;
+    return lane_total + 48u * nfast;
 }
 
 // Process the wave range [lo, hi) of genome [glo, ghi).
