@@ -49,11 +49,11 @@ namespace kf {
 //   variants 12, 13: k = 7 pair counting with 32-byte lanes (K1w, wide_fast),
 //             static wave ranges, one 1024-thread workgroup per CU, ring of
 //             2 / 3 iterations of 2 KiB; for every other k they run as variant 1
-constexpr int kNumVariants = 20;
-constexpr int kDefaultVariant = 18;   // K1x at k = 7; variant 1 (K1) for every other k
+constexpr int kNumVariants = 21;
+constexpr int kDefaultVariant = 20;   // K1x (alternating return checks) at k = 7; variant 1 (K1) for every other k
 constexpr int kFirstPairVariant = 5;
 // K1x default shares by wave age slot (KF_WAVE_WEIGHTS overrides)
-constexpr uint32_t kWaveW0 = 13, kWaveW1 = 10, kWaveW2 = 8, kWaveW3 = 6;
+constexpr uint32_t kWaveW0 = 20, kWaveW1 = 13, kWaveW2 = 9, kWaveW3 = 5;
 #ifndef KF_PAIR_ABL
 #define KF_PAIR_ABL 0
 #endif
@@ -87,7 +87,8 @@ template <> struct WideKnobs<17> { static constexpr int aux = Shape<17>::aux, la
 // K1x: 48-byte lanes (3 KiB per wave iteration), table classification (x_fast)
 template <> struct Shape<18> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 3; };
 template <> struct Shape<19> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };
-template <int V> constexpr bool kX = V == 18 || V == 19;
+template <> struct Shape<20> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // + alternating checks
+template <int V> constexpr bool kX = V == 18 || V == 19 || V == 20;
 template <int V> constexpr bool kStaticPair = V == 10 || V == 11 || kWide<V> || kX<V>;
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
@@ -262,6 +263,12 @@ constexpr uint32_t kFwdSEnd = kPairSBase + (1u << 15);
 __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
     return __hip_atomic_fetch_add((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+
+// Workgroup barrier ordering LDS only: waits for this wave's LDS operations, not
+// for its vector-memory ones (__syncthreads waits for vmcnt(0) too, i.e. for the
+// ring's last prefetches and the flush's row stores, a full memory latency under
+// load; nothing here reads global memory another wave of the workgroup wrote).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // 7-mer (kf code, A0 C1 T2 G3, complement = ^2) -> S slot: the orientation whose
 // middle base (bits 6-7) has bit 7 clear, with that bit dropped.
@@ -694,15 +701,17 @@ constexpr int kWChunk = 2 * kChunk;
 constexpr uint32_t kWideHot = 0xC000C000u;    // a half >= 0x4000
 constexpr uint32_t kWideStep = 0x4000u;
 
-// Move kWideStep out of each hot half of the LDS word at byte address a into the
-// count row until both halves are below 0x2000 (compare-and-swap: exact under
-// concurrent adds).  P word: 8-mers 2w, 2w+1; S word (a >= kPairSBase): forward
-// 7-mers 2w, 2w+1.
+// Move STEP out of each hot half (>= STEP, HOT = the halves' bits at or above it)
+// of the LDS word at byte address a into the count row until both halves are
+// below STEP (compare-and-swap: exact under concurrent adds).  P word: 8-mers 2w,
+// 2w+1; S word (a >= kPairSBase): forward 7-mers 2w, 2w+1.  K1w: STEP 0x4000;
+// K1x: 0x2000 (it checks returns every other iteration, see x_fast).
+template <uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
 __device__ __noinline__ void wide_drain(uint32_t a, const uint32_t* __restrict__ code2col, uint32_t* gcounts) {
     lds_u32* p = (lds_u32*)(uintptr_t)a;
     uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (cur & kWideHot) {
-        const uint32_t sub = ((cur & 0xC0000000u) ? (kWideStep << 16) : 0u) | ((cur & 0xC000u) ? kWideStep : 0u);
+    while (cur & HOT) {
+        const uint32_t sub = ((cur & (HOT & 0xFFFF0000u)) ? (STEP << 16) : 0u) | ((cur & (HOT & 0xFFFFu)) ? STEP : 0u);
         uint32_t seen = cur;
         if (__hip_atomic_compare_exchange_strong(p, &seen, cur - sub, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP)) {
@@ -712,10 +721,10 @@ __device__ __noinline__ void wide_drain(uint32_t a, const uint32_t* __restrict__
                 if (!((sub >> (16 * h)) & 0xFFFFu)) continue;
                 const uint32_t bin = 2 * w + h;
                 if (single) {
-                    atomicAdd(gcounts + code2col[bin], kWideStep);
+                    atomicAdd(gcounts + code2col[bin], STEP);
                 } else {
-                    atomicAdd(gcounts + code2col[bin >> 2], kWideStep);       // older 7-mer
-                    atomicAdd(gcounts + code2col[bin & 0x3FFFu], kWideStep);  // newer 7-mer
+                    atomicAdd(gcounts + code2col[bin >> 2], STEP);       // older 7-mer
+                    atomicAdd(gcounts + code2col[bin & 0x3FFFu], STEP);  // newer 7-mer
                 }
             }
             cur -= sub;
@@ -724,13 +733,16 @@ __device__ __noinline__ void wide_drain(uint32_t a, const uint32_t* __restrict__
         }
     }
 }
+template <uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
 __device__ __noinline__ void wide_scan_drain(const uint32_t* __restrict__ code2col, uint32_t* gcounts, int lane) {
     for (uint32_t w = (uint32_t)lane; w < kFwdSEnd / 4; w += kWave) {
         const uint32_t v = __hip_atomic_load((lds_u32*)(uintptr_t)(4 * w), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (v & kWideHot) wide_drain(4 * w, code2col, gcounts);
+        if (v & HOT) wide_drain<HOT, STEP>(4 * w, code2col, gcounts);
     }
 }
+constexpr uint32_t kXHot = 0xE000E000u;   // K1x: a half >= 0x2000
+constexpr uint32_t kXStep = 0x2000u;
 
 struct WideBlock {
     uint4 a, b;   // lane L: bytes [32L, 32L + 16) and [32L + 16, 32L + 32) of the 2 KiB chunk
@@ -865,7 +877,7 @@ __device__ __forceinline__ bool wide_fast(const WideBlock& d, const CountArgs& A
 
 // Irregular 1 KiB chunk (16-byte lane layout, count_chunk's general path): every
 // counted window as a single into S by its forward code; returns checked at once.
-template <bool MASKED>
+template <bool MASKED, uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
 __device__ __forceinline__ uint32_t wide_singles(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
                                                  const ChunkMask& m, uint64_t iv0, uint32_t carry, uint32_t* gcounts,
                                                  uint32_t& lane_total, uint32_t& drained) {
@@ -883,8 +895,8 @@ __device__ __forceinline__ uint32_t wide_singles(const uint4 d, const CountArgs&
         const uint32_t y = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, 2 * K);
         o |= lds_add_rtn(kPairSBase + ((y >> 1) << 2), ((R >> r) & 1u) * half_one(y));
     }
-    if (__builtin_amdgcn_ballot_w64((o & kWideHot) != 0) != 0) {
-        wide_scan_drain(A.code2col, gcounts, lane);
+    if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
+        wide_scan_drain<HOT, STEP>(A.code2col, gcounts, lane);
         drained = 1;
     }
     lane_total += (uint32_t)__builtin_popcount(R);
@@ -1018,6 +1030,10 @@ __device__ __forceinline__ uint32_t x_zmap(uint32_t x, uint32_t e, uint32_t c) {
 // counted) otherwise.  Returns are checked at the end of the iteration: after a
 // half crosses 0x4000 every wave adds at most one more iteration to it (<= 24 x 64
 // adds) before its own drain, so a half stays below 0x4000 + 16 x 1536 = 0xA000.
+// CHECK = false (K1x with alternating checks, variant 20): adds without returns;
+// the caller checks every other iteration with the 0x2000 threshold, so a half
+// stays below 0x2000 + 16 x 2 x 1536 = 0xE000.
+template <bool CHECK = true, uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
 __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
                                        uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
     constexpr uint32_t TM = (1u << 12) - 1u;
@@ -1100,7 +1116,12 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
         lane_total += a ^ dl;
         rt[j] = 0;
 #else
-        rt[j] = lds_add_rtn(a, dl);
+        if constexpr (CHECK) {
+            rt[j] = lds_add_rtn(a, dl);
+        } else {
+            lds_add(a, dl);
+            rt[j] = 0;
+        }
 #endif
     }
     {
@@ -1119,7 +1140,12 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
         lds_add(a23, d23);
         rt[23] = 0;
 #else
-        rt[23] = lds_add_rtn(a23, d23);
+        if constexpr (CHECK) {
+            rt[23] = lds_add_rtn(a23, d23);
+        } else {
+            lds_add(a23, d23);
+            rt[23] = 0;
+        }
 #endif
     }
     lane_total -= nl;   // + 48 per fast iteration, added by the caller
@@ -1137,12 +1163,14 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
         lane_total += (pad[0] ^ pad[1] ^ pad[2] ^ pad[3]) & 1u;
     }
 #endif
-    uint32_t o = 0;
+    if constexpr (CHECK) {
+        uint32_t o = 0;
 #pragma unroll
-    for (int j = 0; j < 24; j += 3) o |= rt[j] | rt[j + 1] | rt[j + 2];
-    if (__builtin_amdgcn_ballot_w64((o & kWideHot) != 0) != 0) {
-        wide_scan_drain(A.code2col, gcounts, lane);
-        drained = 1;
+        for (int j = 0; j < 24; j += 3) o |= rt[j] | rt[j + 1] | rt[j + 2];
+        if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
+            wide_scan_drain<HOT, STEP>(A.code2col, gcounts, lane);
+            drained = 1;
+        }
     }
     carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)c0, kWave - 1) & TM, 31u, 31u);
     return true;
@@ -1151,9 +1179,13 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
 // The wave range [lo, hi) of genome [glo, ghi) in 3 KiB iterations (K1x).
 // `drained` is set if a u16 half of this range was moved to the count row (the
 // flush then adds with atomics).
-template <int RING>
+// ALT (variant 20, RING = 2): returns checked in ring slot 0 only, with the
+// 0x2000 threshold (every irregular iteration checks too).
+template <int RING, bool ALT = false>
 __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                     uint64_t lo, uint64_t hi, int lane, uint32_t& drained) {
+    static_assert(!ALT || RING == 2, "alternating checks need a 2-slot ring");
+    constexpr uint32_t HOT = ALT ? kXHot : kWideHot, STEP = ALT ? kXStep : kWideStep;
     if (lo >= hi) return 0;
     uint32_t* gcounts = A.counts + (uint64_t)g * A.nbins;
     const uint64_t t_begin = A.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -1163,6 +1195,7 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
 #pragma unroll
     for (int j = 0; j < RING; ++j) buf[j] = x_load(A.bytes, rg.c0, j * kXChunk, rg.end_r, lane);
     rg.warm16<7>(A, lane);
+    __builtin_amdgcn_s_setprio(0);   // (the setup ran at top priority, see count_kernel)
     uint64_t t_loop = 0;
     if (A.prof) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1173,7 +1206,19 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
     const ChunkMask m = rg.mask();
     uint32_t lane_total = 0;
     uint32_t nfast = 0;   // fast iterations (wave-uniform): 48 windows per lane each, less its newlines
-    auto step = [&](const XBlock& bf) {
+#ifdef KF_K1X_PRIO   // experiment: rotate the wave priority every iteration (equal issue share by age slot)
+    uint32_t prio = (uint32_t)(threadIdx.x >> 8);
+#endif
+    auto step = [&](const XBlock& bf, int slot) {
+#ifdef KF_K1X_PRIO
+        prio = (prio + 1) & 3u;
+        switch (prio) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+        }
+#endif
 #if KF_K1W_ABL == 4
         lane_total += bf.q[0].x ^ bf.q[0].w ^ bf.q[1].y ^ bf.q[1].z ^ bf.q[2].x ^ bf.q[2].w;
         rel += kXChunk;
@@ -1185,7 +1230,13 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         const bool m1 = rg.masked(A, rel + kChunk);
         const uint64_t iv1 = rg.iv;
         const bool m2 = rg.masked(A, rel + 2 * kChunk);
-        const bool fast = !(m0 || m1 || m2) && x_fast(bf, A, lane, carry, gcounts, lane_total, drained);
+        bool fast = !(m0 || m1 || m2);
+        if (fast) {
+            if (!ALT || slot == 0)
+                fast = x_fast<true, HOT, STEP>(bf, A, lane, carry, gcounts, lane_total, drained);
+            else
+                fast = x_fast<false, HOT, STEP>(bf, A, lane, carry, gcounts, lane_total, drained);
+        }
         nfast += fast ? 1u : 0u;
         if (!fast) {
             // irregular: the three 1 KiB thirds in 16-byte lane layout, singles into S
@@ -1197,9 +1248,9 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
                 const uint64_t ivh = h == 0 ? iv0 : (h == 1 ? iv1 : rg.iv);
                 const uint4 hb = rg.load(A.bytes, r, lane);
                 if (mh)
-                    carry = wide_singles<true>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
+                    carry = wide_singles<true, HOT, STEP>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
                 else
-                    carry = wide_singles<false>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
+                    carry = wide_singles<false, HOT, STEP>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
             }
         }
         rel += kXChunk;
@@ -1208,7 +1259,7 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
     for (uint32_t i = 0; i + RING <= nx; i += RING) {
 #pragma unroll
         for (int j = 0; j < RING; ++j) {
-            step(buf[j]);
+            step(buf[j], j);
 #if KF_K1W_ABL == 5   // profiling only: every iteration re-reads the range's first chunks (cache hits)
             buf[j] = x_load(A.bytes, rg.c0, (uint32_t)j * kXChunk, rg.end_r, lane);
 #else
@@ -1219,12 +1270,13 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
     const uint32_t rem = nx % RING;
 #pragma unroll
     for (int j = 0; j < RING - 1; ++j)
-        if (rem > (uint32_t)j) step(buf[j]);
+        if (rem > (uint32_t)j) step(buf[j], j);
     if (A.prof && lane == 0) {   // KF_COUNT_PROFILE=1: per-wave-slot loop cycles per 1 KiB chunk
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         const uint64_t t_end = __builtin_amdgcn_s_memtime();
         const int w = (int)(threadIdx.x >> 6);
         atomicAdd(A.prof + 0, (unsigned long long)(t_loop - t_begin));
+        atomicAdd(A.prof + 96 + w, (unsigned long long)(t_loop - t_begin));
         atomicAdd(A.prof + 1, (unsigned long long)(t_end - t_loop));
         atomicAdd(A.prof + 2, 1ull);
         atomicAdd(A.prof + 8 + w, (unsigned long long)(t_end - t_loop));
@@ -1346,6 +1398,9 @@ __global__ void __launch_bounds__(Shape<V>::block)
     int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, span_lo, lane,
                                           [&](uint64_t i) { return A.goff[i + 1]; });
     for (; g < A.n_genomes; ++g) {
+        // K1x: a piece's setup (bounds, interval search, warm-up: dependent loads)
+        // at top priority, so the youngest wave slots do not start late
+        if constexpr (kX<V>) __builtin_amdgcn_s_setprio(3);
         const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
         if (glo >= span_hi) break;
         const uint64_t plo = max(glo, span_lo), phi = min(ghi, span_hi);
@@ -1370,11 +1425,11 @@ __global__ void __launch_bounds__(Shape<V>::block)
         if constexpr (PAIR) {
             uint32_t drained = kX<V> ? 0u : 1u;   // K1x: plain row stores unless a half was drained
             if constexpr (kX<V>)
-                s = process_range_x<Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane, drained);
-            else if constexpr (kWide<V>)
+                s = process_range_x<Shape<V>::ring, V == 20>(A, g, glo, ghi, lo_c, hi_c, lane, drained);
+            if constexpr (kWide<V>)
                 s = process_range_wide<Shape<V>::ring, WideKnobs<V>::aux, WideKnobs<V>::late != 0>(
                     A, g, glo, ghi, lo_c, hi_c, lane);
-            else
+            if constexpr (!kX<V> && !kWide<V>)
                 s = process_range<K, false, 0, Shape<V>::ring, true>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
             const uint64_t t_p0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             // the columns' forward representatives, loaded before the barrier so
@@ -1382,7 +1437,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
             uint32_t rep[8];
 #pragma unroll
             for (int c = 0; c < 8; ++c) rep[c] = A.col2rep[tid + c * kBlock];
-            __syncthreads();   // every add of this piece is done
+            lds_barrier();   // every add of this piece is done
             const uint64_t t_p1 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             uint32_t F[16];
             pair_f_sums(hist, tid, F);
@@ -1392,11 +1447,11 @@ __global__ void __launch_bounds__(Shape<V>::block)
                 F[2 * i] += v & 0xFFFFu;
                 F[2 * i + 1] += v >> 16;
             }
-            __syncthreads();   // P and S read
+            lds_barrier();   // P and S read
 #pragma unroll
             for (int i = 0; i < 8; ++i) *(uint2*)(hist + i * 2048 + 2 * tid) = make_uint2(F[2 * i], F[2 * i + 1]);
             if (lane == 0) hist[16384 + wave] = drained;   // (words past F are free now)
-            __syncthreads();   // F in LDS words [0, 16384), drain flags after it
+            lds_barrier();   // F in LDS words [0, 16384), drain flags after it
             // A whole genome in this span with no drained half: no other workgroup
             // and nothing else touches row g, which the caller zeroed, so it is
             // written with plain stores; otherwise coalesced atomics.
@@ -1416,9 +1471,10 @@ __global__ void __launch_bounds__(Shape<V>::block)
                     __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
-            __syncthreads();   // columns read
+            lds_barrier();   // columns read
             uint4* h4 = (uint4*)hist;
             for (uint32_t i = tid; i < kFwdSEnd / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+            if (A.prof && lane == 0) atomicAdd(A.prof + 80 + wave, (unsigned long long)(t_p1 - t_p0));   // per wave
             if (A.prof && tid == 0) {   // barrier wait of wave 0 and the flush, per piece
                 atomicAdd(A.prof + 3, (unsigned long long)(t_p1 - t_p0));
                 atomicAdd(A.prof + 4, 1ull);
@@ -1473,7 +1529,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
         s = wave_sum(s);
         if constexpr (PAIR) {   // (no LDS left for reduction slots)
             if (lane == 0 && s) atomicAdd(A.totals + g, s);
-            __syncthreads();    // P and S zero before the next piece's adds
+            lds_barrier();    // P and S zero before the next piece's adds
         } else {
             if (lane == 0) red[wave] = s;
             __syncthreads();
@@ -2016,7 +2072,7 @@ void* count_kernel_v(int k) {
 // Variants >= kFirstPairVariant are the pair kernel at k = 7 and variant 1 elsewhere.
 bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant && v <= 7; }
 bool is_dyn(int k, int v) { return k <= kLdsMaxK && (v == 8 || v == 9); }
-bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 19; }
+bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 20; }
 int effective_variant(int k, int v) {
     return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v) && !is_static_pair(k, v)) ? 1 : v;
 }
@@ -2052,6 +2108,7 @@ void* count_kernel_for(int k, int v) {
         case 17: return (void*)&count_kernel<7, 17>;
         case 18: return (void*)&count_kernel<7, 18>;
         case 19: return (void*)&count_kernel<7, 19>;
+        case 20: return (void*)&count_kernel<7, 20>;
         default: return (void*)&count_kernel<7, 10>;
         }
     }
@@ -2188,7 +2245,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.flags = flags;
     const char* pe = getenv("KF_COUNT_PROFILE");   // debugging aid: synchronous, prints to stderr
     if (pe && *pe == '1' && !bucket) {
-        if (hipMalloc((void**)&A.prof, 80 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 80 * 8, s) != hipSuccess ||
+        if (hipMalloc((void**)&A.prof, 112 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 112 * 8, s) != hipSuccess ||
             hipMemsetAsync(A.prof + 42, 0xFF, 8, s) != hipSuccess)
             return kf_fail(KF_EHIP, "profile buffer");
     }
@@ -2204,7 +2261,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (A.prof) {
-        unsigned long long h[80];
+        unsigned long long h[112];
         float ms = 0.f;
         if (hipEventRecord(pe1, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess ||
             hipEventElapsedTime(&ms, pe0, pe1) != hipSuccess ||
@@ -2231,8 +2288,8 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
                         (double)h[56 + x] / (double)h[72 + x] * 1e-5, (double)h[64 + x] * 1e-5);
         for (int w = 0; w < 16; ++w)
             if (h[24 + w])
-                fprintf(stderr, "  wave %2d: %.0f cyc/chunk over %llu chunks\n", w, (double)h[8 + w] / h[24 + w],
-                        h[24 + w]);
+                fprintf(stderr, "  wave %2d: %.0f cyc/chunk over %llu chunks, setup %.3g, barrier wait %.3g cyc/piece\n", w,
+                        (double)h[8 + w] / h[24 + w], h[24 + w], (double)h[96 + w] / nf, (double)h[80 + w] / nf);
     }
     return KF_OK;
 }
