@@ -3,10 +3,11 @@
 # gpurun_out/traffic_k{7,11}.json and profiles/<round>/ (bench.py reads them).
 set -u
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
-ROUND=${ROUND:-r01}
+ROUND=${ROUND:-r02}
+V7=${V7:-20}   # the k=7 default variant (KF_COUNT_VARIANT)
 for k in 7 11; do
-  if [ $k -le 8 ]; then KN="count_kernel<$k, 1>"; else KN="bucket_kernel<$k>"; fi
-  PMC_TAG=pmc_k$k VARIANT=1 GROUPS_LIST=$'FETCH_SIZE\nWRITE_SIZE' AB_ARGS="--k $k" bash "$REPO/tools/pmc_variant.sh" || exit $?
+  if [ $k -le 8 ]; then KN="count_kernel<$k, $V7>"; else KN="bucket_kernel<$k>"; fi
+  PMC_TAG=pmc_k$k VARIANT=$V7 GROUPS_LIST=$'FETCH_SIZE\nWRITE_SIZE' AB_ARGS="--k $k" bash "$REPO/tools/pmc_variant.sh" || exit $?
   python3 "$REPO/tools/pmc_traffic.py" "$REPO/gpurun_out/pmc_k$k" --kernel "$KN" --k $k \
       --out "$REPO/gpurun_out/traffic_k$k.json" || exit $?
   mkdir -p "$REPO/profiles/$ROUND" && cp "$REPO/gpurun_out/traffic_k$k.json" "$REPO/profiles/$ROUND/"
