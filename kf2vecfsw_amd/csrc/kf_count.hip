@@ -1224,13 +1224,8 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         rel += kXChunk;
         return;
 #endif
-        // interval cursor before each 1 KiB third (a later test may advance it)
-        const bool m0 = rg.masked(A, rel);
-        const uint64_t iv0 = rg.iv;
-        const bool m1 = rg.masked(A, rel + kChunk);
-        const uint64_t iv1 = rg.iv;
-        const bool m2 = rg.masked(A, rel + 2 * kChunk);
-        bool fast = !(m0 || m1 || m2);
+        // one test for the whole 3 KiB (range edges, excluded intervals)
+        bool fast = !rg.masked_span(A, rel, kXChunk);
         if (fast) {
             if (!ALT || slot == 0)
                 fast = x_fast<true, HOT, STEP>(bf, A, lane, carry, gcounts, lane_total, drained);
@@ -1239,6 +1234,12 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         }
         nfast += fast ? 1u : 0u;
         if (!fast) {
+            // interval cursor before each 1 KiB third (a later test may advance it)
+            const bool m0 = rg.masked(A, rel);
+            const uint64_t iv0 = rg.iv;
+            const bool m1 = rg.masked(A, rel + kChunk);
+            const uint64_t iv1 = rg.iv;
+            const bool m2 = rg.masked(A, rel + 2 * kChunk);
             // irregular: the three 1 KiB thirds in 16-byte lane layout, singles into S
 #pragma unroll
             for (int h = 0; h < 3; ++h) {

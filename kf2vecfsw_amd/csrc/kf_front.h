@@ -453,6 +453,11 @@ struct Range {
         }
         return ivs_r < rel + kChunk || rel < lo_r || rel + kChunk > hi_r;
     }
+    // as masked, for the span [rel, rel + len) (len a multiple of kChunk)
+    __device__ __forceinline__ bool masked_span(const CountArgs& A, uint32_t rel, uint32_t len) {
+        if (rel >= ive_r) return masked(A, rel) || ivs_r < rel + len || rel + len > hi_r;
+        return ivs_r < rel + len || rel < lo_r || rel + len > hi_r;
+    }
     __device__ __forceinline__ ChunkMask mask() const { return ChunkMask{glo, lo, hi}; }
     __device__ __forceinline__ uint4 load(const uint8_t* bytes, uint32_t rel, int lane) const {
         return load_chunk(bytes, c0, rel, end_r, lane);
