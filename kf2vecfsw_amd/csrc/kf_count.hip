@@ -1018,6 +1018,12 @@ __device__ __forceinline__ XBlock x_load(const uint8_t* bytes, uint64_t c0, uint
     return b;
 }
 
+// dot4 weights of word i's bytes t = 0..3 in the newline test: 96 - (4i + t)
+__device__ __forceinline__ constexpr uint32_t x_nl_weights(int i) {
+    return (uint32_t)(96 - 4 * i) | (uint32_t)(95 - 4 * i) << 8 | (uint32_t)(94 - 4 * i) << 16 |
+           (uint32_t)(93 - 4 * i) << 24;
+}
+
 // z = bits other than 5 (c = 1): x ^ e; bit 5 (c = 0): x & ~e  (one v_bitop3)
 __device__ __forceinline__ uint32_t x_zmap(uint32_t x, uint32_t e, uint32_t c) {
     uint32_t r;
@@ -1057,29 +1063,30 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
         const uint32_t t01 = (pc[b] << 8) | pc[b + 1], t23 = (pc[b + 2] << 8) | pc[b + 3];
         C[i] = (t01 << 15) | (t23 >> 1);
     }
-    // newline flags (low bit of z), 8 bytes per byte of the mask: bit r = entry r
-    uint32_t g[6];
+    // Newline and bad-byte test in one dot4 chain: byte b (entry 47 - b) weighs
+    // 96 - b, so V = sum z_b (96 - b) is 0 without a newline, 49 + e for one
+    // newline at entry e, and >= 98 otherwise (every nonzero z adds >= 49: two
+    // newlines, or one bad byte's z >= 2).
+    uint32_t va = 0u, vb = 0u;
 #pragma unroll
-    for (int q = 0; q < 6; ++q)
-        g[q] = __builtin_amdgcn_udot4(z[2 * q], 0x10204080u, __builtin_amdgcn_udot4(z[2 * q + 1], 0x01020408u, 0u, false),
-                                      false);
-    const uint32_t NL1 = __builtin_amdgcn_perm(g[0], g[1], 0x0C0C0400u);   // entries 32..47
-    const uint32_t NL0 = (__builtin_amdgcn_perm(g[2], g[3], 0x0C0C0400u) << 16) | __builtin_amdgcn_perm(g[4], g[5], 0x0C0C0400u);
-    const uint32_t bz = ((z[0] | z[1] | z[2]) | (z[3] | z[4] | z[5])) | ((z[6] | z[7] | z[8]) | (z[9] | z[10] | z[11]));
-    const uint32_t nl = (uint32_t)__builtin_popcount(NL0) + (uint32_t)__builtin_popcount(NL1);
-    const bool self_ok = ((bz & 0xFEFEFEFEu) | (nl & ~1u)) == 0;
+    for (int i = 0; i < 6; ++i) {
+        va = __builtin_amdgcn_udot4(z[i], x_nl_weights(i), va, false);
+        vb = __builtin_amdgcn_udot4(z[i + 6], x_nl_weights(i + 6), vb, false);
+    }
+    const uint32_t V = va + vb;
+    uint32_t nl;   // min(V, 1), opaque: the compiler would turn its uses into selects (v_cndmask)
+    asm("v_min_u32_e32 %0, 1, %1" : "=v"(nl) : "v"(V));
     carry = __builtin_amdgcn_readfirstlane(carry);   // wave-uniform: its tests run on the SALU
-    if (t_n(carry) < 6u || __builtin_amdgcn_ballot_w64(!self_ok) != 0) return false;
-    // drop the newline entry: entries below it stay, every entry above moves down one
-    const uint64_t M = (((uint64_t)NL1 << 32) | NL0) - 1u;   // entries below the newline (all if none)
-    const uint32_t ML = (uint32_t)M, MH = (uint32_t)(M >> 32);
-    const uint32_t m0 = ML & 0xFFFFu, m1 = ML >> 16, m2 = MH & 0xFFFFu;
-    const uint32_t E0 = m0 | (m0 << __builtin_popcount(m0));
-    const uint32_t E1 = m1 | (m1 << __builtin_popcount(m1));
-    const uint32_t E2 = m2 | (m2 << __builtin_popcount(m2));
-    const uint32_t c0 = bfi(E0, C[0], __builtin_amdgcn_alignbit(C[1], C[0], 2));
-    const uint32_t c1 = bfi(E1, C[1], __builtin_amdgcn_alignbit(C[2], C[1], 2));
-    const uint32_t c2 = bfi(E2, C[2], C[2] >> 2);
+    if (t_n(carry) < 6u || __builtin_amdgcn_ballot_w64(V >= 98u) != 0) return false;
+    // drop the newline entry: entries below it stay, every entry above moves down
+    // one.  Region r (entries 16r..16r+15) keeps its low q_r = clamp(2e - 32r, 0, 32)
+    // bits; without a newline 2V - 98 wraps high and every region keeps all.
+    const uint32_t e2 = 2u * V - 98u;
+    const uint32_t q0 = min(e2, 32u), q1 = min(max(e2, 32u), 64u) - 32u, q2 = min(max(e2, 64u), 96u) - 64u;
+    const uint32_t L0 = (uint32_t)(~0ull << q0), L1 = (uint32_t)(~0ull << q1), L2 = (uint32_t)(~0ull << q2);
+    const uint32_t c0 = bfi(L0, __builtin_amdgcn_alignbit(C[1], C[0], 2), C[0]);
+    const uint32_t c1 = bfi(L1, __builtin_amdgcn_alignbit(C[2], C[1], 2), C[1]);
+    const uint32_t c2 = bfi(L2, C[2] >> 2, C[2]);
     // context: lane L-1's newest entries (lane 0: the carry) above this lane's
     // n = 48 - nl entries: W = pC << 2n | (c2 : c1 : c0)
     const uint32_t pC = wave_shr1(t_codes(carry), c0);
@@ -1183,7 +1190,8 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
 // 0x2000 threshold (every irregular iteration checks too).
 template <int RING, bool ALT = false>
 __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
-                                                    uint64_t lo, uint64_t hi, int lane, uint32_t& drained) {
+                                                    uint64_t lo, uint64_t hi, int lane, uint32_t& drained,
+                                                    uint32_t piece = 0) {
     static_assert(!ALT || RING == 2, "alternating checks need a 2-slot ring");
     constexpr uint32_t HOT = ALT ? kXHot : kWideHot, STEP = ALT ? kXStep : kWideStep;
     if (lo >= hi) return 0;
@@ -1282,6 +1290,12 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         atomicAdd(A.prof + 2, 1ull);
         atomicAdd(A.prof + 8 + w, (unsigned long long)(t_end - t_loop));
         atomicAdd(A.prof + 24 + w, (unsigned long long)rg.nch);
+        if (blockIdx.x == 0 && piece < 8) {   // timeline of workgroup 0: setup start, loop start, loop end
+            unsigned long long* tr = A.prof + 112 + (piece * 16 + w) * 8;
+            tr[1] = t_begin;
+            tr[2] = t_loop;
+            tr[3] = t_end;
+        }
     }
     return lane_total + 48u * nfast;
 }
@@ -1398,7 +1412,11 @@ __global__ void __launch_bounds__(Shape<V>::block)
     // first genome whose end is beyond span_lo
     int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, span_lo, lane,
                                           [&](uint64_t i) { return A.goff[i + 1]; });
+    uint32_t npiece = 0;   // (KF_COUNT_PROFILE timeline)
+    const uint32_t fr_lo = kX<V> ? wave_frac((uint32_t)wave, A.wave_w) : 0u;
+    const uint32_t fr_hi = kX<V> ? wave_frac((uint32_t)wave + 1, A.wave_w) : 0u;
     for (; g < A.n_genomes; ++g) {
+        const uint64_t t_top = A.prof ? __builtin_amdgcn_s_memtime() : 0;
         // K1x: a piece's setup (bounds, interval search, warm-up: dependent loads)
         // at top priority, so the youngest wave slots do not start late
         if constexpr (kX<V>) __builtin_amdgcn_s_setprio(3);
@@ -1409,8 +1427,8 @@ __global__ void __launch_bounds__(Shape<V>::block)
         // wave w owns [split(w), split(w+1)): 16-byte aligned, monotone, covering [plo, phi)
         uint64_t lo_c, hi_c;
         if constexpr (kX<V>) {   // K1x: parts weighted by wave slot (KF_WAVE_WEIGHTS)
-            lo_c = split_at_w(plo, phi, (uint32_t)wave, A.wave_w);
-            hi_c = split_at_w(plo, phi, (uint32_t)wave + 1, A.wave_w);
+            lo_c = split_at_frac(plo, phi, fr_lo);
+            hi_c = split_at_frac(plo, phi, fr_hi);
         } else {
             lo_c = split_at(plo, phi, wave, kWaves);
             hi_c = split_at(plo, phi, wave + 1, kWaves);
@@ -1426,7 +1444,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
         if constexpr (PAIR) {
             uint32_t drained = kX<V> ? 0u : 1u;   // K1x: plain row stores unless a half was drained
             if constexpr (kX<V>)
-                s = process_range_x<Shape<V>::ring, V == 20>(A, g, glo, ghi, lo_c, hi_c, lane, drained);
+                s = process_range_x<Shape<V>::ring, V == 20>(A, g, glo, ghi, lo_c, hi_c, lane, drained, npiece);
             if constexpr (kWide<V>)
                 s = process_range_wide<Shape<V>::ring, WideKnobs<V>::aux, WideKnobs<V>::late != 0>(
                     A, g, glo, ghi, lo_c, hi_c, lane);
@@ -1476,6 +1494,14 @@ __global__ void __launch_bounds__(Shape<V>::block)
             uint4* h4 = (uint4*)hist;
             for (uint32_t i = tid; i < kFwdSEnd / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
             if (A.prof && lane == 0) atomicAdd(A.prof + 80 + wave, (unsigned long long)(t_p1 - t_p0));   // per wave
+            if (A.prof && lane == 0 && blockIdx.x == 0 && npiece < 8) {
+                unsigned long long* tr = A.prof + 112 + (npiece * 16 + wave) * 8;
+                tr[0] = t_top;
+                tr[4] = t_p0;
+                tr[5] = t_p1;
+                tr[6] = __builtin_amdgcn_s_memtime();
+            }
+            ++npiece;
             if (A.prof && tid == 0) {   // barrier wait of wave 0 and the flush, per piece
                 atomicAdd(A.prof + 3, (unsigned long long)(t_p1 - t_p0));
                 atomicAdd(A.prof + 4, 1ull);
@@ -2246,7 +2272,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.flags = flags;
     const char* pe = getenv("KF_COUNT_PROFILE");   // debugging aid: synchronous, prints to stderr
     if (pe && *pe == '1' && !bucket) {
-        if (hipMalloc((void**)&A.prof, 112 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 112 * 8, s) != hipSuccess ||
+        if (hipMalloc((void**)&A.prof, 1152 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 1152 * 8, s) != hipSuccess ||
             hipMemsetAsync(A.prof + 42, 0xFF, 8, s) != hipSuccess)
             return kf_fail(KF_EHIP, "profile buffer");
     }
@@ -2262,7 +2288,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (A.prof) {
-        unsigned long long h[112];
+        static unsigned long long h[1152];
         float ms = 0.f;
         if (hipEventRecord(pe1, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess ||
             hipEventElapsedTime(&ms, pe0, pe1) != hipSuccess ||
@@ -2287,6 +2313,20 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
             if (h[72 + x])
                 fprintf(stderr, "  XCC %d: %llu workgroups, lifetime mean %.3f max %.3f ms\n", x, h[72 + x],
                         (double)h[56 + x] / (double)h[72 + x] * 1e-5, (double)h[64 + x] * 1e-5);
+        const char* tl = getenv("KF_COUNT_TIMELINE");   // per-piece timeline of workgroup 0 (cycles from its start)
+        if (tl && *tl == '1') {
+            const unsigned long long z = h[112];
+            for (int pc = 0; pc < 8; ++pc) {
+                if (!h[112 + pc * 16 * 8]) break;
+                fprintf(stderr, "  piece %d (top, setup, loop, end, barrier-in, barrier-out, flushed) per wave:\n", pc);
+                for (int w = 0; w < 16; ++w) {
+                    const unsigned long long* t = h + 112 + (pc * 16 + w) * 8;
+                    fprintf(stderr, "    w%2d", w);
+                    for (int q = 0; q < 7; ++q) fprintf(stderr, " %9lld", t[q] ? (long long)(t[q] - z) : -1ll);
+                    fprintf(stderr, "\n");
+                }
+            }
+        }
         for (int w = 0; w < 16; ++w)
             if (h[24 + w])
                 fprintf(stderr, "  wave %2d: %.0f cyc/chunk over %llu chunks, setup %.3g, barrier wait %.3g cyc/piece\n", w,

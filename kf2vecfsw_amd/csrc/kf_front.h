@@ -476,9 +476,12 @@ __device__ __forceinline__ uint64_t split_at(uint64_t plo, uint64_t phi, uint64_
 // As split_at with wave w's part proportional to byte (w >> 2) of `wts` (the
 // wave's age slot on its SIMD: the SIMD issues oldest-first, so slot 0 runs
 // fastest); n = 16.  wts = 0x01010101 is an equal split.
-__device__ __forceinline__ uint64_t split_at_w(uint64_t plo, uint64_t phi, uint32_t w, uint32_t wts) {
-    if (w == 0) return plo;
-    if (w >= 16) return phi;
+//   Split once per kernel into a 2^-20 fixed-point fraction (wave_frac), then per
+// piece one 64-bit multiply (split_at_frac): a 64x32/32 division per wave and
+// piece is a long SALU sequence that the CU's 16 waves serialise on.
+__device__ __forceinline__ uint32_t wave_frac(uint32_t w, uint32_t wts) {
+    if (w == 0) return 0u;
+    if (w >= 16) return 1u << 20;
     const uint32_t b0 = wts & 0xFFu, b1 = (wts >> 8) & 0xFFu, b2 = (wts >> 16) & 0xFFu, b3 = wts >> 24;
     const uint32_t tot = 4u * (b0 + b1 + b2 + b3);
     // prefix weight of waves 0..w-1: full slots below w's slot plus w's own slot members
@@ -488,9 +491,14 @@ __device__ __forceinline__ uint64_t split_at_w(uint64_t plo, uint64_t phi, uint3
     cum += (s > 1 ? 4u * b1 : (s == 1 ? r * b1 : 0u));
     cum += (s > 2 ? 4u * b2 : (s == 2 ? r * b2 : 0u));
     cum += (s == 3 ? r * b3 : 0u);
-    const uint64_t len = phi - plo;
-    const uint64_t q = (uint64_t)(((unsigned __int128)len * cum) / tot);
-    const uint64_t x = (plo + q) & ~(uint64_t)15;
+    return (cum << 20) / tot;   // cum <= 1020: no overflow
+}
+
+// [plo, phi) at fraction fr / 2^20 (phi - plo < 2^44), 16-byte aligned; the
+// same fr gives the same point, so adjacent waves' parts are monotone and covering.
+__device__ __forceinline__ uint64_t split_at_frac(uint64_t plo, uint64_t phi, uint32_t fr) {
+    if (fr >= (1u << 20)) return phi;
+    const uint64_t x = (plo + (((phi - plo) * fr) >> 20)) & ~(uint64_t)15;
     return min(max(x, plo), phi);
 }
 
