@@ -53,7 +53,7 @@ constexpr int kNumVariants = 21;
 constexpr int kDefaultVariant = 20;   // K1x (alternating return checks) at k = 7; variant 1 (K1) for every other k
 constexpr int kFirstPairVariant = 5;
 // K1x default shares by wave age slot (KF_WAVE_WEIGHTS overrides)
-constexpr uint32_t kWaveW0 = 20, kWaveW1 = 13, kWaveW2 = 9, kWaveW3 = 5;
+constexpr uint32_t kWaveW0 = 20, kWaveW1 = 17, kWaveW2 = 11, kWaveW3 = 6;
 #ifndef KF_PAIR_ABL
 #define KF_PAIR_ABL 0
 #endif
@@ -1018,10 +1018,10 @@ __device__ __forceinline__ XBlock x_load(const uint8_t* bytes, uint64_t c0, uint
     return b;
 }
 
-// dot4 weights of word i's bytes t = 0..3 in the newline test: 96 - (4i + t)
+// dot4 weights of word i's bytes t = 0..3 in the newline test: 2 (96 - (4i + t))
 __device__ __forceinline__ constexpr uint32_t x_nl_weights(int i) {
-    return (uint32_t)(96 - 4 * i) | (uint32_t)(95 - 4 * i) << 8 | (uint32_t)(94 - 4 * i) << 16 |
-           (uint32_t)(93 - 4 * i) << 24;
+    return (uint32_t)(192 - 8 * i) | (uint32_t)(190 - 8 * i) << 8 | (uint32_t)(188 - 8 * i) << 16 |
+           (uint32_t)(186 - 8 * i) << 24;
 }
 
 // z = bits other than 5 (c = 1): x ^ e; bit 5 (c = 0): x & ~e  (one v_bitop3)
@@ -1052,37 +1052,36 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
         const uint32_t x = w[i];
         const uint32_t e = __builtin_amdgcn_perm(kXTabHi, kXTabLo, x & 0x07070707u);
         z[i] = x_zmap(x, e, cdf);
-        pc[i] = __builtin_amdgcn_udot4(x & 0x06060606u, 0x01041040u, 0u, false);   // 2 x packed codes
+        // 2 x packed codes; odd words accumulate onto the even word's, shifted up one byte
+        pc[i] = __builtin_amdgcn_udot4(x & 0x06060606u, 0x01041040u, (i & 1) ? pc[i - 1] << 8 : 0u, false);
     }
     // codes: C2 = entries 32..47 (bytes 0..15), C1 = 16..31, C0 = 0..15 (entry 0 = byte 47)
-    // (pc < 512 and even: pc[b] << 8 | pc[b + 1] is twice the 16-bit code of 8 bases)
+    // (pc[b + 1] = pc[b] << 8 + dot4 of word b + 1 is twice the 16-bit code of 8 bases)
     uint32_t C[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const int b = 4 * (2 - i);
-        const uint32_t t01 = (pc[b] << 8) | pc[b + 1], t23 = (pc[b + 2] << 8) | pc[b + 3];
-        C[i] = (t01 << 15) | (t23 >> 1);
+        C[i] = (pc[b + 1] << 15) | (pc[b + 3] >> 1);
     }
     // Newline and bad-byte test in one dot4 chain: byte b (entry 47 - b) weighs
-    // 96 - b, so V = sum z_b (96 - b) is 0 without a newline, 49 + e for one
-    // newline at entry e, and >= 98 otherwise (every nonzero z adds >= 49: two
-    // newlines, or one bad byte's z >= 2).
-    uint32_t va = 0u, vb = 0u;
+    // 2 (96 - b), so V = sum z_b 2 (96 - b) is 0 without a newline, 98 + 2e for
+    // one newline at entry e, and >= 196 otherwise (every nonzero z adds >= 98:
+    // two newlines, or one bad byte's z >= 2).
+    uint32_t va[4] = {0u, 0u, 0u, 0u};   // four chains of three: a short dependent path
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        va = __builtin_amdgcn_udot4(z[i], x_nl_weights(i), va, false);
-        vb = __builtin_amdgcn_udot4(z[i + 6], x_nl_weights(i + 6), vb, false);
-    }
-    const uint32_t V = va + vb;
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) va[c] = __builtin_amdgcn_udot4(z[3 * c + i], x_nl_weights(3 * c + i), va[c], false);
+    const uint32_t V = (va[0] + va[1]) + (va[2] + va[3]);
     uint32_t nl;   // min(V, 1), opaque: the compiler would turn its uses into selects (v_cndmask)
     asm("v_min_u32_e32 %0, 1, %1" : "=v"(nl) : "v"(V));
     carry = __builtin_amdgcn_readfirstlane(carry);   // wave-uniform: its tests run on the SALU
-    if (t_n(carry) < 6u || __builtin_amdgcn_ballot_w64(V >= 98u) != 0) return false;
+    if (t_n(carry) < 6u || __builtin_amdgcn_ballot_w64(V >= 196u) != 0) return false;
     // drop the newline entry: entries below it stay, every entry above moves down
     // one.  Region r (entries 16r..16r+15) keeps its low q_r = clamp(2e - 32r, 0, 32)
-    // bits; without a newline 2V - 98 wraps high and every region keeps all.
-    const uint32_t e2 = 2u * V - 98u;
-    const uint32_t q0 = min(e2, 32u), q1 = min(max(e2, 32u), 64u) - 32u, q2 = min(max(e2, 64u), 96u) - 64u;
+    // bits; without a newline V - 98 wraps high and every region keeps all.
+    const uint32_t e2 = V - 98u;
+    const uint32_t q0 = min(e2, 32u), q1 = min(max(e2, 32u), 64u) - 32u, q2 = min(max(e2, 64u) - 64u, 32u);
     const uint32_t L0 = (uint32_t)(~0ull << q0), L1 = (uint32_t)(~0ull << q1), L2 = (uint32_t)(~0ull << q2);
     const uint32_t c0 = bfi(L0, __builtin_amdgcn_alignbit(C[1], C[0], 2), C[0]);
     const uint32_t c1 = bfi(L1, __builtin_amdgcn_alignbit(C[2], C[1], 2), C[1]);
@@ -1235,7 +1234,11 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         // one test for the whole 3 KiB (range edges, excluded intervals)
         bool fast = !rg.masked_span(A, rel, kXChunk);
         if (fast) {
+#ifdef KF_K1X_NOCHECK   // profiling only (unsafe on low-complexity input): no u16 return checks
+            if (false)
+#else
             if (!ALT || slot == 0)
+#endif
                 fast = x_fast<true, HOT, STEP>(bf, A, lane, carry, gcounts, lane_total, drained);
             else
                 fast = x_fast<false, HOT, STEP>(bf, A, lane, carry, gcounts, lane_total, drained);

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--n-period", type=int, default=0)
+    ap.add_argument("--weights", default="", help="';'-separated KF_WAVE_WEIGHTS sets, alternated per round")
     args = ap.parse_args()
     import torch
     from kf2vecfsw_amd import counter as C
@@ -32,12 +33,17 @@ def main():
     db = C.synth_device_batch(args.genomes, args.seq_len, 20260101, n_period=args.n_period, device=dev)
     kc = C.KmerCounter(args.k, dev)
     fasta = int(db.off[-1].item())
-    variants = [int(v) for v in args.variants.split(",")]
+    wsets = args.weights.split(";") if args.weights else [""]
+    variants = [(int(v), w) for v in args.variants.split(",") for w in wsets]
     times = {v: [] for v in variants}
     ref = None
     for r in range(args.rounds):
-        for v in variants:
+        for v, w in variants:
             os.environ["KF_COUNT_VARIANT"] = str(v)
+            if w:
+                os.environ["KF_WAVE_WEIGHTS"] = w
+            else:
+                os.environ.pop("KF_WAVE_WEIGHTS", None)
             cnt, tot = kc.alloc_out(args.genomes)
             kc.count(db, cnt, tot)  # warm (also selects/caches the variant's grid)
             torch.cuda.synchronize()
@@ -53,7 +59,7 @@ def main():
                 b.record()
                 evs.append((a, b))
             torch.cuda.synchronize()
-            times[v] += [a.elapsed_time(b) for a, b in evs]
+            times[(v, w)] += [a.elapsed_time(b) for a, b in evs]
             h = C.counts_to_numpy(cnt)
             if ref is None:
                 ref = h
@@ -62,7 +68,7 @@ def main():
     out = {}
     for v in variants:
         t = np.array(times[v])
-        out[v] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+        out[f"{v[0]}" + (f"/{v[1]}" if v[1] else "")] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
                   "GBps_median": fasta / (np.median(t) * 1e-3) / 1e9,
                   "Gbases_s": args.genomes * args.seq_len / (np.median(t) * 1e-3) / 1e9,
                   "grid": kc.launch_info() if False else None}
