@@ -49,7 +49,7 @@ namespace kf {
 //   variants 12, 13: k = 7 pair counting with 32-byte lanes (K1w, wide_fast),
 //             static wave ranges, one 1024-thread workgroup per CU, ring of
 //             2 / 3 iterations of 2 KiB; for every other k they run as variant 1
-constexpr int kNumVariants = 21;
+constexpr int kNumVariants = 22;
 constexpr int kDefaultVariant = 20;   // K1x (alternating return checks) at k = 7; variant 1 (K1) for every other k
 constexpr int kFirstPairVariant = 5;
 // K1x default shares by wave age slot (KF_WAVE_WEIGHTS overrides)
@@ -88,7 +88,8 @@ template <> struct WideKnobs<17> { static constexpr int aux = Shape<17>::aux, la
 template <> struct Shape<18> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 3; };
 template <> struct Shape<19> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };
 template <> struct Shape<20> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // + alternating checks
-template <int V> constexpr bool kX = V == 18 || V == 19 || V == 20;
+template <> struct Shape<21> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // + paired iterations
+template <int V> constexpr bool kX = V >= 18 && V <= 21;
 template <int V> constexpr bool kStaticPair = V == 10 || V == 11 || kWide<V> || kX<V>;
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
@@ -428,6 +429,12 @@ __device__ __forceinline__ uint32_t u16sum2(uint32_t w) { return (w & 0xFFFFu) +
 // Flush step 1 (1024 threads): per forward 7-mer y, F(y) = sum_a P[4y + a] +
 // sum_a P[a 4^7 + y]; thread t owns y = 2048 i + 2t + {0, 1}, i = 0..7
 // (lane-consecutive reads).
+// LDS word of F(y) in the flush: bits 1-4 XOR bits 8-11.  A wave reads F at 64
+// representatives y that differ in their low bases and at their reverse
+// complements, which then differ only in bits 8-13: unswizzled, every rc read
+// of a wave would hit one bank.  Bit 0 is kept, so F(2m), F(2m+1) stay a pair.
+__device__ __forceinline__ uint32_t f_swz(uint32_t y) { return y ^ (((y >> 8) & 15u) << 1); }
+
 __device__ __forceinline__ void pair_f_sums(const uint32_t* hist, int tid, uint32_t (&F)[16]) {
     const uint4* h4 = (const uint4*)hist;
 #pragma unroll
@@ -1039,10 +1046,12 @@ __device__ __forceinline__ uint32_t x_zmap(uint32_t x, uint32_t e, uint32_t c) {
 // CHECK = false (K1x with alternating checks, variant 20): adds without returns;
 // the caller checks every other iteration with the 0x2000 threshold, so a half
 // stays below 0x2000 + 16 x 2 x 1536 = 0xE000.
-template <bool CHECK = true, uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
-__device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
-                                       uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
-    constexpr uint32_t TM = (1u << 12) - 1u;
+// Classification of a 3 KiB block: the packed codes of each lane's 48 bytes
+// (newline entry not yet removed) and the newline / bad-byte sum V.
+struct XCls {
+    uint32_t C[3], V;
+};
+__device__ __forceinline__ XCls x_cls(const XBlock& d) {
     const uint32_t w[12] = {d.q[0].x, d.q[0].y, d.q[0].z, d.q[0].w, d.q[1].x, d.q[1].y,
                             d.q[1].z, d.q[1].w, d.q[2].x, d.q[2].y, d.q[2].z, d.q[2].w};
     const uint32_t cdf = 0xDFDFDFDFu;
@@ -1073,10 +1082,21 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
 #pragma unroll
         for (int c = 0; c < 4; ++c) va[c] = __builtin_amdgcn_udot4(z[3 * c + i], x_nl_weights(3 * c + i), va[c], false);
     const uint32_t V = (va[0] + va[1]) + (va[2] + va[3]);
+    XCls r;
+    r.C[0] = C[0], r.C[1] = C[1], r.C[2] = C[2], r.V = V;
+    return r;
+}
+
+// Counting half of a fast iteration (the caller has tested V < 196 in every lane
+// and a complete carry): newline removal, context, the 24 pair adds.  Returns the
+// OR of the adds' returns (CHECK) for the caller's u16 test; updates the carry.
+template <bool CHECK>
+__device__ __forceinline__ uint32_t x_body(const XCls& k, uint32_t& carry, uint32_t& lane_total) {
+    constexpr uint32_t TM = (1u << 12) - 1u;
+    const uint32_t V = k.V;
+    const uint32_t C[3] = {k.C[0], k.C[1], k.C[2]};
     uint32_t nl;   // min(V, 1), opaque: the compiler would turn its uses into selects (v_cndmask)
     asm("v_min_u32_e32 %0, 1, %1" : "=v"(nl) : "v"(V));
-    carry = __builtin_amdgcn_readfirstlane(carry);   // wave-uniform: its tests run on the SALU
-    if (t_n(carry) < 6u || __builtin_amdgcn_ballot_w64(V >= 196u) != 0) return false;
     // drop the newline entry: entries below it stay, every entry above moves down
     // one.  Region r (entries 16r..16r+15) keeps its low q_r = clamp(2e - 32r, 0, 32)
     // bits; without a newline V - 98 wraps high and every region keeps all.
@@ -1155,8 +1175,26 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
 #endif
     }
     lane_total -= nl;   // + 48 per fast iteration, added by the caller
+    uint32_t o = 0;
+    if constexpr (CHECK) {
+#pragma unroll
+        for (int j = 0; j < 24; j += 3) o |= rt[j] | rt[j + 1] | rt[j + 2];
+    }
+    carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)c0, kWave - 1) & TM, 31u, 31u);
+    return o;
+}
+
+template <bool CHECK = true, uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
+__device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
+                                       uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
+    const XCls k = x_cls(d);
+    carry = __builtin_amdgcn_readfirstlane(carry);   // wave-uniform: its tests run on the SALU
+    if (t_n(carry) < 6u || __builtin_amdgcn_ballot_w64(k.V >= 196u) != 0) return false;
+    const uint32_t o = x_body<CHECK>(k, carry, lane_total);
 #ifdef KF_K1X_PAD   // profiling only: N extra VALU ops of one kind (1 = v_xor VOP2, 2 = v_perm VOP3)
     {
+        const uint32_t w[12] = {d.q[0].x, d.q[0].y, d.q[0].z, d.q[0].w, d.q[1].x, d.q[1].y,
+                                d.q[1].z, d.q[1].w, d.q[2].x, d.q[2].y, d.q[2].z, d.q[2].w};
         uint32_t pad[4] = {w[0], w[1], w[2], w[3]};   // four independent chains
 #pragma unroll
         for (int i = 0; i < KF_K1X_PAD_N; ++i) {
@@ -1169,16 +1207,10 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
         lane_total += (pad[0] ^ pad[1] ^ pad[2] ^ pad[3]) & 1u;
     }
 #endif
-    if constexpr (CHECK) {
-        uint32_t o = 0;
-#pragma unroll
-        for (int j = 0; j < 24; j += 3) o |= rt[j] | rt[j + 1] | rt[j + 2];
-        if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
-            wide_scan_drain<HOT, STEP>(A.code2col, gcounts, lane);
-            drained = 1;
-        }
+    if (CHECK && __builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
+        wide_scan_drain<HOT, STEP>(A.code2col, gcounts, lane);
+        drained = 1;
     }
-    carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)c0, kWave - 1) & TM, 31u, 31u);
     return true;
 }
 
@@ -1187,12 +1219,18 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
 // flush then adds with atomics).
 // ALT (variant 20, RING = 2): returns checked in ring slot 0 only, with the
 // 0x2000 threshold (every irregular iteration checks too).
-template <int RING, bool ALT = false>
+// PAIRED (variant 21, RING = 2): two fast iterations at a time when both pass
+// (classification of both first, then both refills, then both bodies, with one
+// u16 test of all 48 returns, threshold 0x2000), else one at a time.  Every add's
+// return is tested, at most two iterations after the add, so a half stays below
+// 0x2000 + 16 x 2 x 1536 = 0xE000.
+template <int RING, bool ALT = false, bool PAIRED = false>
 __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                     uint64_t lo, uint64_t hi, int lane, uint32_t& drained,
                                                     uint32_t piece = 0) {
     static_assert(!ALT || RING == 2, "alternating checks need a 2-slot ring");
-    constexpr uint32_t HOT = ALT ? kXHot : kWideHot, STEP = ALT ? kXStep : kWideStep;
+    static_assert(!PAIRED || (RING == 2 && !ALT), "paired iterations need a 2-slot ring");
+    constexpr uint32_t HOT = (ALT || PAIRED) ? kXHot : kWideHot, STEP = (ALT || PAIRED) ? kXStep : kWideStep;
     if (lo >= hi) return 0;
     uint32_t* gcounts = A.counts + (uint64_t)g * A.nbins;
     const uint64_t t_begin = A.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -1269,6 +1307,25 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
     };
     const uint32_t nx = (rg.nch + 2) / 3;   // 3 KiB iterations
     for (uint32_t i = 0; i + RING <= nx; i += RING) {
+        if constexpr (PAIRED) {
+            if (!rg.masked_span(A, rel, 2 * kXChunk)) {
+                const XCls k0 = x_cls(buf[0]), k1 = x_cls(buf[1]);
+                carry = __builtin_amdgcn_readfirstlane(carry);
+                if (t_n(carry) >= 6u && __builtin_amdgcn_ballot_w64(max(k0.V, k1.V) >= 196u) == 0) {
+                    // both raw blocks are consumed: refill the ring before the bodies
+                    buf[0] = x_load(A.bytes, rg.c0, rel + 2 * kXChunk, rg.end_r, lane);
+                    buf[1] = x_load(A.bytes, rg.c0, rel + 3 * kXChunk, rg.end_r, lane);
+                    const uint32_t o = x_body<true>(k0, carry, lane_total) | x_body<true>(k1, carry, lane_total);
+                    if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
+                        wide_scan_drain<HOT, STEP>(A.code2col, gcounts, lane);
+                        drained = 1;
+                    }
+                    nfast += 2;
+                    rel += 2 * kXChunk;
+                    continue;
+                }
+            }
+        }
 #pragma unroll
         for (int j = 0; j < RING; ++j) {
             step(buf[j], j);
@@ -1294,7 +1351,7 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         atomicAdd(A.prof + 8 + w, (unsigned long long)(t_end - t_loop));
         atomicAdd(A.prof + 24 + w, (unsigned long long)rg.nch);
         if (blockIdx.x == 0 && piece < 8) {   // timeline of workgroup 0: setup start, loop start, loop end
-            unsigned long long* tr = A.prof + 112 + (piece * 16 + w) * 8;
+            unsigned long long* tr = A.prof + 112 + (piece * 16 + w) * 16;
             tr[1] = t_begin;
             tr[2] = t_loop;
             tr[3] = t_end;
@@ -1447,7 +1504,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
         if constexpr (PAIR) {
             uint32_t drained = kX<V> ? 0u : 1u;   // K1x: plain row stores unless a half was drained
             if constexpr (kX<V>)
-                s = process_range_x<Shape<V>::ring, V == 20>(A, g, glo, ghi, lo_c, hi_c, lane, drained, npiece);
+                s = process_range_x<Shape<V>::ring, V == 20, V == 21>(A, g, glo, ghi, lo_c, hi_c, lane, drained, npiece);
             if constexpr (kWide<V>)
                 s = process_range_wide<Shape<V>::ring, WideKnobs<V>::aux, WideKnobs<V>::late != 0>(
                     A, g, glo, ghi, lo_c, hi_c, lane);
@@ -1455,10 +1512,20 @@ __global__ void __launch_bounds__(Shape<V>::block)
                 s = process_range<K, false, 0, Shape<V>::ring, true>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
             const uint64_t t_p0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             // the columns' forward representatives, loaded before the barrier so
-            // their latency overlaps it
+            // their latency overlaps it.  A whole genome (the common case) takes
+            // four consecutive columns per lane and 16-byte row stores (the flush
+            // is bound by the CU's store issue); other pieces one column per lane
+            // and coalesced atomics.
+            const bool whole = plo == glo && phi == ghi && !(A.flags & KF_ACCUMULATE);
             uint32_t rep[8];
+            if (whole) {
+                const uint4 r0 = *(const uint4*)(A.col2rep + 4 * tid), r1 = *(const uint4*)(A.col2rep + 4096 + 4 * tid);
+                rep[0] = r0.x, rep[1] = r0.y, rep[2] = r0.z, rep[3] = r0.w;
+                rep[4] = r1.x, rep[5] = r1.y, rep[6] = r1.z, rep[7] = r1.w;
+            } else {
 #pragma unroll
-            for (int c = 0; c < 8; ++c) rep[c] = A.col2rep[tid + c * kBlock];
+                for (int c = 0; c < 8; ++c) rep[c] = A.col2rep[tid + c * kBlock];
+            }
             lds_barrier();   // every add of this piece is done
             const uint64_t t_p1 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             uint32_t F[16];
@@ -1469,11 +1536,14 @@ __global__ void __launch_bounds__(Shape<V>::block)
                 F[2 * i] += v & 0xFFFFu;
                 F[2 * i + 1] += v >> 16;
             }
+            const uint64_t t_q0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             lds_barrier();   // P and S read
+            const uint64_t t_q1 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) *(uint2*)(hist + i * 2048 + 2 * tid) = make_uint2(F[2 * i], F[2 * i + 1]);
+            for (int i = 0; i < 8; ++i) *(uint2*)(hist + f_swz(i * 2048 + 2 * tid)) = make_uint2(F[2 * i], F[2 * i + 1]);
             if (lane == 0) hist[16384 + wave] = drained;   // (words past F are free now)
             lds_barrier();   // F in LDS words [0, 16384), drain flags after it
+            const uint64_t t_q2 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             // A whole genome in this span with no drained half: no other workgroup
             // and nothing else touches row g, which the caller zeroed, so it is
             // written with plain stores; otherwise coalesced atomics.
@@ -1481,28 +1551,41 @@ __global__ void __launch_bounds__(Shape<V>::block)
             const uint4 f0 = fl[0], f1 = fl[1], f2 = fl[2], f3 = fl[3];
             const bool any_drain = (f0.x | f0.y | f0.z | f0.w | f1.x | f1.y | f1.z | f1.w | f2.x | f2.y | f2.z | f2.w |
                                     f3.x | f3.y | f3.z | f3.w) != 0;
-            const bool store = plo == glo && phi == ghi && !any_drain && !(A.flags & KF_ACCUMULATE);
+            uint32_t cv[8];
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-                const uint32_t col = tid + c * kBlock;
                 const uint32_t y = rep[c], rc = kf_revcomp<K>(y);
-                const uint32_t v = hist[y] + hist[rc];
-                if (store) {
-                    if (v) gc[col] = v;
-                } else if (v) {
-                    __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
+                cv[c] = hist[f_swz(y)] + hist[f_swz(rc)];
             }
+            const uint64_t t_q3 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             lds_barrier();   // columns read
+            const uint64_t t_q4 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
             uint4* h4 = (uint4*)hist;
             for (uint32_t i = tid; i < kFwdSEnd / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+            // the row writes last: their issue overlaps the zeroing, the barrier
+            // and the next piece's setup
+            if (whole && !any_drain) {
+                *(uint4*)(gc + 4 * tid) = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+                *(uint4*)(gc + 4096 + 4 * tid) = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+            } else {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t col = whole ? (c >> 2) * 4096 + 4 * tid + (c & 3) : tid + c * kBlock;
+                    if (cv[c]) __hip_atomic_fetch_add(gc + col, cv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
             if (A.prof && lane == 0) atomicAdd(A.prof + 80 + wave, (unsigned long long)(t_p1 - t_p0));   // per wave
             if (A.prof && lane == 0 && blockIdx.x == 0 && npiece < 8) {
-                unsigned long long* tr = A.prof + 112 + (npiece * 16 + wave) * 8;
+                unsigned long long* tr = A.prof + 112 + (npiece * 16 + wave) * 16;
                 tr[0] = t_top;
                 tr[4] = t_p0;
                 tr[5] = t_p1;
-                tr[6] = __builtin_amdgcn_s_memtime();
+                tr[6] = t_q0;
+                tr[7] = t_q1;
+                tr[8] = t_q2;
+                tr[9] = t_q3;
+                tr[10] = t_q4;
+                tr[11] = __builtin_amdgcn_s_memtime();
             }
             ++npiece;
             if (A.prof && tid == 0) {   // barrier wait of wave 0 and the flush, per piece
@@ -2102,7 +2185,7 @@ void* count_kernel_v(int k) {
 // Variants >= kFirstPairVariant are the pair kernel at k = 7 and variant 1 elsewhere.
 bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant && v <= 7; }
 bool is_dyn(int k, int v) { return k <= kLdsMaxK && (v == 8 || v == 9); }
-bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 20; }
+bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 21; }
 int effective_variant(int k, int v) {
     return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v) && !is_static_pair(k, v)) ? 1 : v;
 }
@@ -2139,6 +2222,7 @@ void* count_kernel_for(int k, int v) {
         case 18: return (void*)&count_kernel<7, 18>;
         case 19: return (void*)&count_kernel<7, 19>;
         case 20: return (void*)&count_kernel<7, 20>;
+        case 21: return (void*)&count_kernel<7, 21>;
         default: return (void*)&count_kernel<7, 10>;
         }
     }
@@ -2275,7 +2359,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.flags = flags;
     const char* pe = getenv("KF_COUNT_PROFILE");   // debugging aid: synchronous, prints to stderr
     if (pe && *pe == '1' && !bucket) {
-        if (hipMalloc((void**)&A.prof, 1152 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 1152 * 8, s) != hipSuccess ||
+        if (hipMalloc((void**)&A.prof, 2304 * 8) != hipSuccess || hipMemsetAsync(A.prof, 0, 2304 * 8, s) != hipSuccess ||
             hipMemsetAsync(A.prof + 42, 0xFF, 8, s) != hipSuccess)
             return kf_fail(KF_EHIP, "profile buffer");
     }
@@ -2291,7 +2375,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (A.prof) {
-        static unsigned long long h[1152];
+        static unsigned long long h[2304];
         float ms = 0.f;
         if (hipEventRecord(pe1, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess ||
             hipEventElapsedTime(&ms, pe0, pe1) != hipSuccess ||
@@ -2320,12 +2404,13 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
         if (tl && *tl == '1') {
             const unsigned long long z = h[112];
             for (int pc = 0; pc < 8; ++pc) {
-                if (!h[112 + pc * 16 * 8]) break;
-                fprintf(stderr, "  piece %d (top, setup, loop, end, barrier-in, barrier-out, flushed) per wave:\n", pc);
+                if (!h[112 + pc * 16 * 16]) break;
+                fprintf(stderr, "  piece %d (top, setup, loop, end, barrier-in, barrier-out, sums, P read, F written, "
+                        "columns, columns read, zeroed) per wave:\n", pc);
                 for (int w = 0; w < 16; ++w) {
-                    const unsigned long long* t = h + 112 + (pc * 16 + w) * 8;
+                    const unsigned long long* t = h + 112 + (pc * 16 + w) * 16;
                     fprintf(stderr, "    w%2d", w);
-                    for (int q = 0; q < 7; ++q) fprintf(stderr, " %9lld", t[q] ? (long long)(t[q] - z) : -1ll);
+                    for (int q = 0; q < 12; ++q) fprintf(stderr, " %9lld", t[q] ? (long long)(t[q] - z) : -1ll);
                     fprintf(stderr, "\n");
                 }
             }

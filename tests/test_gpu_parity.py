@@ -360,7 +360,7 @@ def test_arbitrary_byte_values(torch_dev, oracle, k):
     check_against_oracle(oracle, blobs, k, counts, totals, fmt=1, tag="bytes")
 
 
-@pytest.mark.parametrize("variant", [5, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20])
+@pytest.mark.parametrize("variant", [5, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
 def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, variant):
     """k=7 pair kernels (5: self-contained chunks, 10: static wave ranges, 12/13:
     32-byte lanes): their
@@ -389,7 +389,7 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, 
     check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16-many")
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20])
+@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
 def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
     """k=7 pair kernels (KF_COUNT_VARIANT 5, 6, 7: self-contained chunks, prefetch
     ring 6 / 4 / 8; 10, 11: static wave ranges, ring 6 / 8; 12, 13: 32-byte lanes,

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--n-period", type=int, default=0)
+    ap.add_argument("--accumulate", action="store_true", help="zero outside the events, accumulate=True")
     ap.add_argument("--weights", default="", help="';'-separated KF_WAVE_WEIGHTS sets, alternated per round")
     args = ap.parse_args()
     import torch
@@ -48,14 +49,13 @@ def main():
             kc.count(db, cnt, tot)  # warm (also selects/caches the variant's grid)
             torch.cuda.synchronize()
             evs = []
-            zero_first = args.k <= 8   # as bench.py: k >= 9 (bucket kernels) write rows whole
             for _ in range(args.reps):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                if zero_first:
+                if args.accumulate:   # count-matrix memset outside the events, atomics-only flushes
                     cnt.zero_()
                     tot.zero_()
                 a.record()
-                kc.count(db, cnt, tot, accumulate=zero_first)
+                kc.count(db, cnt, tot, accumulate=args.accumulate)   # default: the CLI's and bench.py's call
                 b.record()
                 evs.append((a, b))
             torch.cuda.synchronize()
