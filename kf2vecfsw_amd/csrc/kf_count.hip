@@ -2157,6 +2157,9 @@ __global__ void __launch_bounds__(1024) stream_probe_kernel(const uint8_t* bytes
 
 }  // namespace kf
 
+#ifdef KF_QUICK_ISA   // tools/isa.sh: one kernel's ISA without the whole variant zoo
+template __global__ void kf::count_kernel<7, KF_QUICK_ISA>(kf::CountArgs);
+#else
 // ====================================================================== C-ABI
 using namespace kf;
 
@@ -2452,3 +2455,4 @@ extern "C" int kf_synth_fasta(uint8_t* d_bytes, const uint64_t* d_goff, int32_t 
     if (hipGetLastError() != hipSuccess) return kf_fail(KF_EHIP, "synth kernel launch failed");
     return KF_OK;
 }
+#endif  // KF_QUICK_ISA

@@ -401,3 +401,15 @@ def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
                               crlf_rate=0.05, poly_rate=0.01) for _ in range(20)]
     counts, totals = run_batch(blobs, 7, torch_dev)
     check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"v{variant}")
+
+
+@pytest.mark.parametrize("variant", [20])
+def test_k7_many_pieces_many_records(torch_dev, oracle, monkeypatch, variant):
+    """Several genome pieces per workgroup, each with many records (excluded
+    intervals), N runs and empty genomes."""
+    monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
+    rng = np.random.default_rng(2026 + variant)
+    blobs = [gen.random_fasta(rng, int(rng.integers(0, 40000)) if i % 37 else 0, max_records=40, n_rate=0.003,
+                              lower=0.05, crlf_rate=0.02, poly_rate=0.01) for i in range(700)]
+    counts, totals = run_batch(blobs, 7, torch_dev)
+    check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"pieces-v{variant}")
