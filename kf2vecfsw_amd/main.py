@@ -88,9 +88,75 @@ def _batches(paths: list[str], budget: int) -> list[list[int]]:
     return out
 
 
+def shard_files(sizes: list[int], samples: list[str], world: int) -> list[list[int]]:
+    """Byte-balanced shards of the input files for `world` GPUs (section 8(e): genomes
+    are independent, no collective).  Files of one sample name stay in one shard,
+    so the reference's last-file-wins rule for duplicate names (main.py:357 writes
+    in input order) holds inside that shard; groups go largest first to the least
+    loaded shard; each shard keeps the input order."""
+    groups: dict[str, list[int]] = {}
+    for i, s in enumerate(samples):
+        groups.setdefault(s, []).append(i)
+    load = [0] * world
+    out: list[list[int]] = [[] for _ in range(world)]
+    for g in sorted(groups.values(), key=lambda g: (-sum(sizes[i] for i in g), g[0])):
+        r = min(range(world), key=lambda r: (load[r], r))
+        out[r].extend(g)
+        load[r] += sum(sizes[i] for i in g)
+    return [sorted(o) for o in out]
+
+
+def _shard_spec(args) -> tuple[int, int] | None:
+    """(rank, world) when this process counts one shard: a child of `-gpus N`
+    (KF_SHARD="r,N") or one rank of torchrun (RANK / WORLD_SIZE, no -gpus)."""
+    e = os.environ.get("KF_SHARD")
+    if e:
+        r, w = (int(x) for x in e.split(","))
+        return r, w
+    if getattr(args, "gpus", 1) == 1 and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return int(os.environ.get("RANK", "0")), int(os.environ["WORLD_SIZE"])
+    return None
+
+
+def _spawn_shards(argv: list[str], world: int) -> int:
+    """`-gpus N`: one child process per GPU (cuda:r), each counting shard r; no
+    data crosses between them (each writes its own genomes' .kf files).  The
+    parent never touches the GPU (KF_SHARD_DEVICE=cuda:0 puts every child on one
+    GPU, for rehearsal on a one-GPU box)."""
+    import subprocess
+    procs = []
+    for r in range(world):
+        pkg_parent = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        env = dict(os.environ, KF_SHARD=f"{r},{world}",
+                   PYTHONPATH=os.pathsep.join(filter(None, [pkg_parent, os.environ.get("PYTHONPATH")])))
+        dev = os.environ.get("KF_SHARD_DEVICE") or f"cuda:{r}"
+        procs.append(subprocess.Popen([sys.executable, "-m", "kf2vecfsw_amd.main"] + argv + ["-device", dev], env=env))
+    return max(abs(p.wait()) for p in procs)
+
+
 def get_frequencies(args) -> None:
-    """kf2vec/main.py:250-373 on the GPU."""
-    print("\n==> Starting k-mer counting for {}\n".format(args.input_dir))
+    """kf2vec/main.py:250-373 on the GPU (-gpus N: byte-balanced file shards, one
+    process per GPU)."""
+    shard = _shard_spec(args)
+    lead = shard is None or shard[0] == 0
+    if shard is None and getattr(args, "gpus", 1) != 1:
+        world = args.gpus
+        if world <= 0:
+            import torch
+            world = max(1, torch.cuda.device_count())   # (counting devices does not initialise them)
+        if world > 1:
+            print("\n==> Starting k-mer counting for {}\n".format(args.input_dir))
+            for d in (args.input_dir, args.output_dir):
+                if not os.path.exists(d):
+                    print("No such directory '{}'".format(d), file=sys.stderr)
+                    sys.exit(0)
+            rc = _spawn_shards(_child_argv(args), world)
+            if rc:
+                sys.exit(rc)
+            print("\n==> Done processing {}".format(args.input_dir))
+            return
+    if lead and not os.environ.get("KF_SHARD"):
+        print("\n==> Starting k-mer counting for {}\n".format(args.input_dir))
 
     if not os.path.exists(args.input_dir):            # main.py:255-259 (exit status 0, as the reference)
         print("No such directory '{}'".format(args.input_dir), file=sys.stderr)
@@ -100,6 +166,11 @@ def get_frequencies(args) -> None:
         sys.exit(0)
 
     files_names, samples_names = list_inputs(args.input_dir)
+    if shard is not None:
+        sizes = [os.path.getsize(os.path.join(args.input_dir, f)) for f in files_names]
+        mine = shard_files(sizes, samples_names, shard[1])[shard[0]]
+        files_names = [files_names[i] for i in mine]
+        samples_names = [samples_names[i] for i in mine]
     if args.k not in supported_k:
         # reference: UnboundLocalError at main.py:327 for k without a vocab branch
         raise ValueError("k={} has no vocabulary: supported k are {}..{}".format(
@@ -108,7 +179,11 @@ def get_frequencies(args) -> None:
     import torch
     from .counter import KmerCounter, pack_files, to_device
 
-    device = torch.device(getattr(args, "device", None) or "cuda")
+    dflt = f"cuda:{os.environ.get('LOCAL_RANK', '0')}" if shard is not None else "cuda"
+    device = torch.device(getattr(args, "device", None) or dflt)
+    if not files_names:   # an empty shard
+        _finish(args, shard, lead)
+        return
     counter = KmerCounter(args.k, device)
     paths = [os.path.join(args.input_dir, f) for f in files_names]
     batches = _batches(paths, _pipeline_budget(paths, getattr(args, "batch_gb", None)))
@@ -223,7 +298,34 @@ def get_frequencies(args) -> None:
         import json
         print(json.dumps({"kf_trace": tr, "total_ms": now_ms()}), file=sys.stderr)
 
-    print("\n==> Done processing {}".format(args.input_dir))
+    _finish(args, shard, lead)
+
+
+def _finish(args, shard, lead: bool) -> None:
+    """torchrun ranks meet in a gloo barrier (host only, nothing crosses) so rank 0
+    prints the reference's last line after every shard is written."""
+    if shard is not None and not os.environ.get("KF_SHARD"):
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+        dist.barrier()
+    if lead and not os.environ.get("KF_SHARD"):
+        print("\n==> Done processing {}".format(args.input_dir))
+
+
+def _child_argv(args) -> list[str]:
+    """The get_frequencies command line of a -gpus child (its shard and device
+    come from KF_SHARD and -device)."""
+    a = ["get_frequencies", "-input_dir", args.input_dir, "-output_dir", args.output_dir, "-k", str(args.k),
+         "-p", str(args.p)]
+    if args.pseudocount:
+        a.append("-pseudocount")
+    if args.raw_cnt:
+        a.append("-raw_cnt")
+    if getattr(args, "batch_gb", None):
+        a += ["-batch_gb", str(args.batch_gb)]
+    return a
 
 
 # ---------------------------------------------------------------------------
@@ -413,6 +515,9 @@ def build_parser() -> argparse.ArgumentParser:
     pf.add_argument("-batch_gb", type=float, default=None,
                     help="Input bytes per device batch (GiB). Default: about 1/8 of the input, 16 MiB..4 GiB")
     pf.add_argument("-device", default=None, help="torch device (default: cuda)")
+    pf.add_argument("-gpus", type=int, default=1,
+                    help="GPUs to shard the files over, one process each (0 = every visible GPU). Default: 1. "
+                         "Under torchrun each rank counts its own shard.")
     pf.set_defaults(func=get_frequencies)
 
     pk = sub.add_parser("get_kmers", description="Extract kmers and frequencies from FASTA files")

@@ -53,3 +53,43 @@ def test_round_robin_shards_cover_all_genomes(world):
     for rank, ids, tmax, gathered in res:
         assert ids == list(range(rank, n * world, world))  # round robin
         assert tmax == 0.5 + (world - 1)                    # max over ranks
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_cli_file_shards_balanced_and_grouped(world):
+    """get_frequencies -gpus N / torchrun: every file in exactly one shard, files of
+    one sample name together (last-file-wins stays inside a shard), shards in input
+    order, and byte loads within one largest group of each other."""
+    import numpy as np
+    from kf2vecfsw_amd.main import shard_files
+    rng = np.random.default_rng(world)
+    sizes = [int(x) for x in rng.integers(1, 10_000_000, size=97)]
+    samples = [f"s{int(i)}" for i in rng.integers(0, 80, size=97)]
+    shards = shard_files(sizes, samples, world)
+    assert len(shards) == world
+    assert sorted(i for sh in shards for i in sh) == list(range(97))
+    for sh in shards:
+        assert sh == sorted(sh)
+    owner = {}
+    for r, sh in enumerate(shards):
+        for i in sh:
+            assert owner.setdefault(samples[i], r) == r
+    loads = [sum(sizes[i] for i in sh) for sh in shards]
+    biggest = max(sum(sizes[i] for i in range(97) if samples[i] == s) for s in set(samples))
+    assert max(loads) - min(loads) <= biggest
+
+
+def test_cli_shard_spec_from_env(monkeypatch):
+    from types import SimpleNamespace
+    from kf2vecfsw_amd.main import _shard_spec, build_parser
+    a = build_parser().parse_args(["get_frequencies", "-input_dir", "i", "-output_dir", "o", "-gpus", "4"])
+    assert a.gpus == 4
+    monkeypatch.delenv("KF_SHARD", raising=False)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert _shard_spec(SimpleNamespace(gpus=1)) is None
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("RANK", "2")
+    assert _shard_spec(SimpleNamespace(gpus=1)) == (2, 4)       # a torchrun rank
+    assert _shard_spec(SimpleNamespace(gpus=4)) is None         # -gpus spawns its own children
+    monkeypatch.setenv("KF_SHARD", "3,8")
+    assert _shard_spec(SimpleNamespace(gpus=1)) == (3, 8)       # a -gpus child

@@ -9,6 +9,8 @@ import pytest
 
 import gen
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 pytestmark = pytest.mark.gpu
 
 
@@ -197,6 +199,34 @@ def test_cli_end_to_end_toy(torch_dev, toy, tmp_path):
     for name, sample, data, exp in toy:
         assert (out / (sample + ".kf")).read_bytes() == exp, sample
     assert sorted(os.listdir(out)) == sorted(t[1] + ".kf" for t in toy)
+
+
+def test_cli_gpus_shards_equal_single_gpu(torch_dev, oracle, tmp_path, monkeypatch):
+    """`get_frequencies -gpus 3` (three child processes, here all on cuda:0 via
+    KF_SHARD_DEVICE) writes the same `.kf` files as one GPU, including a sample name
+    shared by two files (the later file wins, as in the reference)."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(77)
+    inp, o1, o3 = tmp_path / "in", tmp_path / "o1", tmp_path / "o3"
+    for d in (inp, o1, o3):
+        d.mkdir()
+    for i in range(11):
+        (inp / f"g{i}.fna").write_bytes(gen.random_fasta(rng, int(rng.integers(1000, 200000)), max_records=4,
+                                                         n_rate=0.001))
+    (inp / "g3.fasta").write_bytes(gen.random_fasta(rng, 5000))   # same sample "g3" as g3.fna
+    env = dict(os.environ, KF_SHARD_DEVICE="cuda:0")
+    base = [sys.executable, "-m", "kf2vecfsw_amd.main", "get_frequencies", "-input_dir", str(inp), "-k", "7",
+            "-p", "2"]
+    r1 = subprocess.run(base + ["-output_dir", str(o1)], env=env, capture_output=True, text=True, timeout=300,
+                        cwd=ROOT)
+    r3 = subprocess.run(base + ["-output_dir", str(o3), "-gpus", "3"], env=env, capture_output=True, text=True,
+                        timeout=300, cwd=ROOT)
+    assert r1.returncode == 0 and r3.returncode == 0, (r1.stderr, r3.stderr)
+    assert sorted(os.listdir(o1)) == sorted(os.listdir(o3)) and len(os.listdir(o1)) == 11
+    for f in os.listdir(o1):
+        assert (o1 / f).read_bytes() == (o3 / f).read_bytes(), f
+    assert sorted(r1.stdout.splitlines()) == sorted(r3.stdout.splitlines())   # same lines, any shard order
 
 
 @pytest.mark.parametrize("k", [7, 11])
