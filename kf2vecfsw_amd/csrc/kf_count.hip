@@ -26,6 +26,8 @@
 #include <stdlib.h>
 
 #include <cstdio>
+#include <map>
+#include <utility>
 
 #include "kf_front.h"
 #include "kf_internal.h"
@@ -49,7 +51,11 @@ namespace kf {
 //   variants 12, 13: k = 7 pair counting with 32-byte lanes (K1w, wide_fast),
 //             static wave ranges, one 1024-thread workgroup per CU, ring of
 //             2 / 3 iterations of 2 KiB; for every other k they run as variant 1
-constexpr int kNumVariants = 22;
+//   variant 22: K1x variant 20 whose waves split only the first part of each
+//             genome piece statically and claim the rest in small units from a
+//             per-workgroup ticket (KF_DYN_FRAC, KF_DYN_UNIT), so they finish a
+//             piece together
+constexpr int kNumVariants = 23;
 constexpr int kDefaultVariant = 20;   // K1x (alternating return checks) at k = 7; variant 1 (K1) for every other k
 constexpr int kFirstPairVariant = 5;
 // K1x default shares by wave age slot (KF_WAVE_WEIGHTS overrides)
@@ -89,7 +95,8 @@ template <> struct Shape<18> { static constexpr int block = 1024, wpe = 4, abl =
 template <> struct Shape<19> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };
 template <> struct Shape<20> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // + alternating checks
 template <> struct Shape<21> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // + paired iterations
-template <int V> constexpr bool kX = V >= 18 && V <= 21;
+template <> struct Shape<22> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // 20 + claimed tail units
+template <int V> constexpr bool kX = V >= 18 && V <= 22;
 template <int V> constexpr bool kStaticPair = V == 10 || V == 11 || kWide<V> || kX<V>;
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
@@ -1227,7 +1234,7 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
 template <int RING, bool ALT = false, bool PAIRED = false>
 __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                     uint64_t lo, uint64_t hi, int lane, uint32_t& drained,
-                                                    uint32_t piece = 0) {
+                                                    uint32_t piece = 0, IvHint* hint = nullptr) {
     static_assert(!ALT || RING == 2, "alternating checks need a 2-slot ring");
     static_assert(!PAIRED || (RING == 2 && !ALT), "paired iterations need a 2-slot ring");
     constexpr uint32_t HOT = (ALT || PAIRED) ? kXHot : kWideHot, STEP = (ALT || PAIRED) ? kXStep : kWideStep;
@@ -1239,7 +1246,10 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
     XBlock buf[RING];
 #pragma unroll
     for (int j = 0; j < RING; ++j) buf[j] = x_load(A.bytes, rg.c0, j * kXChunk, rg.end_r, lane);
-    rg.warm16<7>(A, lane);
+    rg.warm16<7>(A, lane, hint);
+    // the cursor as it stands at the range start (the loop's tests of a last
+    // iteration's thirds may advance it past intervals beyond the range end)
+    if (hint) *hint = rg.hint();
     __builtin_amdgcn_s_setprio(0);   // (the setup ran at top priority, see count_kernel)
     uint64_t t_loop = 0;
     if (A.prof) {
@@ -1453,6 +1463,12 @@ __global__ void __launch_bounds__(Shape<V>::block)
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     constexpr uint32_t NCODES = PAIR ? kFwdSEnd / 4 : (GLOBAL ? 4u : ModeOf<K>::lds_codes);
+    // variant 22: this workgroup's claim ticket as the previous launch left it
+    // (read by every wave before the barrier below, which precedes every claim)
+    uint32_t claim_base = 0;
+    if constexpr (V == 22)
+        claim_base = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(A.claim + blockIdx.x * kClaimStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (!GLOBAL) {
         for (uint32_t i = tid; i < NCODES; i += kBlock) hist[i] = 0;
         __syncthreads();
@@ -1486,9 +1502,11 @@ __global__ void __launch_bounds__(Shape<V>::block)
         if (phi <= plo) continue;
         // wave w owns [split(w), split(w+1)): 16-byte aligned, monotone, covering [plo, phi)
         uint64_t lo_c, hi_c;
+        // variant 22: [plo, dlo) is split by wave slot, [dlo, phi) claimed in units
+        const uint64_t dlo = V == 22 ? split_at_frac(plo, phi, A.dyn_frac) : phi;
         if constexpr (kX<V>) {   // K1x: parts weighted by wave slot (KF_WAVE_WEIGHTS)
-            lo_c = split_at_frac(plo, phi, fr_lo);
-            hi_c = split_at_frac(plo, phi, fr_hi);
+            lo_c = split_at_frac(plo, dlo, fr_lo);
+            hi_c = split_at_frac(plo, dlo, fr_hi);
         } else {
             lo_c = split_at(plo, phi, wave, kWaves);
             hi_c = split_at(plo, phi, wave + 1, kWaves);
@@ -1503,8 +1521,39 @@ __global__ void __launch_bounds__(Shape<V>::block)
         uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
         if constexpr (PAIR) {
             uint32_t drained = kX<V> ? 0u : 1u;   // K1x: plain row stores unless a half was drained
-            if constexpr (kX<V>)
-                s = process_range_x<Shape<V>::ring, V == 20, V == 21>(A, g, glo, ghi, lo_c, hi_c, lane, drained, npiece);
+            if constexpr (kX<V>) {
+                // variant 22: after its static part each wave claims units of
+                // [dlo, phi) by ticket until it draws one past the last unit, so
+                // every piece takes exactly nunits + kWaves tickets and the next
+                // piece's base is known to all waves (one call site of the loop)
+                const uint32_t U = A.dyn_unit;
+                const uint32_t nunits = V == 22 ? (uint32_t)((phi - dlo + U - 1) / U) : 0u;
+                // In the claimed phase the next ticket is drawn before the current
+                // unit is counted (its return latency hides under the unit), and
+                // the interval cursor passes from range to range (no search).
+                uint64_t rlo = lo_c, rhi = hi_c;
+                uint32_t* const tk = A.claim + blockIdx.x * kClaimStride;
+                IvHint hint{0, 0, 0, false};
+                bool claimed = false;
+                uint32_t t_next = 0;
+                s = 0;
+                for (;;) {
+                    if (V == 22 && claimed && lane == 0)
+                        t_next = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s += process_range_x<Shape<V>::ring, V == 20 || V == 22, V == 21>(
+                        A, g, glo, ghi, rlo, rhi, lane, drained, npiece, V == 22 ? &hint : nullptr);
+                    if constexpr (V != 22) break;
+                    if (!claimed && lane == 0)
+                        t_next = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    claimed = true;
+                    const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)t_next) - claim_base;
+                    if (u >= nunits) break;
+                    rlo = dlo + (uint64_t)u * U;
+                    rhi = min(rlo + U, phi);
+                    __builtin_amdgcn_s_setprio(3);
+                }
+                if constexpr (V == 22) claim_base += nunits + (uint32_t)kWaves;
+            }
             if constexpr (kWide<V>)
                 s = process_range_wide<Shape<V>::ring, WideKnobs<V>::aux, WideKnobs<V>::late != 0>(
                     A, g, glo, ghi, lo_c, hi_c, lane);
@@ -2188,7 +2237,7 @@ void* count_kernel_v(int k) {
 // Variants >= kFirstPairVariant are the pair kernel at k = 7 and variant 1 elsewhere.
 bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant && v <= 7; }
 bool is_dyn(int k, int v) { return k <= kLdsMaxK && (v == 8 || v == 9); }
-bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 21; }
+bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 22; }
 int effective_variant(int k, int v) {
     return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v) && !is_static_pair(k, v)) ? 1 : v;
 }
@@ -2226,6 +2275,7 @@ void* count_kernel_for(int k, int v) {
         case 19: return (void*)&count_kernel<7, 19>;
         case 20: return (void*)&count_kernel<7, 20>;
         case 21: return (void*)&count_kernel<7, 21>;
+        case 22: return (void*)&count_kernel<7, 22>;
         default: return (void*)&count_kernel<7, 10>;
         }
     }
@@ -2255,6 +2305,42 @@ int current_variant() {
     if (!e || !*e) return kDefaultVariant;
     const int v = atoi(e);
     return (v >= 0 && v < kNumVariants) ? v : kDefaultVariant;
+}
+
+// Variant 22's claim tickets: one u32 per workgroup (kClaimStride apart), per
+// device and stream, allocated and zeroed on first use; a launch continues from
+// the values the previous launch on that stream left, so nothing is reset per launch.
+constexpr int kClaimMaxGrid = 1024;
+uint32_t* claim_buffer(int dev, hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, uint32_t*> bufs;
+    std::lock_guard<std::mutex> lk(mu);
+    uint32_t*& p = bufs[{dev, s}];
+    if (!p) {
+        const size_t n = (size_t)kClaimMaxGrid * kClaimStride * sizeof(uint32_t);
+        if (hipMalloc((void**)&p, n) != hipSuccess) return p = nullptr;
+        if (hipMemset(p, 0, n) != hipSuccess) {
+            (void)hipFree(p);
+            return p = nullptr;
+        }
+    }
+    return p;
+}
+
+// KF_DYN_FRAC (0..1, default 0.85): statically split share of a piece (variant 22);
+// KF_DYN_UNIT (3 KiB iterations per claimed unit, 1..64, default 2).
+uint32_t dyn_frac() {
+    const char* e = getenv("KF_DYN_FRAC");
+    double f = (e && *e) ? atof(e) : 0.85;
+    if (!(f >= 0.0)) f = 0.0;
+    if (f > 1.0) f = 1.0;
+    return (uint32_t)(f * (double)(1u << 20));
+}
+uint32_t dyn_unit() {
+    const char* e = getenv("KF_DYN_UNIT");
+    int n = (e && *e) ? atoi(e) : 2;
+    if (n < 1 || n > 64) n = 2;
+    return (uint32_t)n * (uint32_t)kXChunk;
 }
 
 // KF_WAVE_WEIGHTS="a0,a1,a2,a3" (tuning/A-B knob, read per launch), each 1..255:
@@ -2375,6 +2461,15 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     if (A.prof && (hipEventCreate(&pe0) != hipSuccess || hipEventCreate(&pe1) != hipSuccess ||
                    hipEventRecord(pe0, s) != hipSuccess))
         return kf_fail(KF_EHIP, "profile events");
+    A.claim = nullptr;
+    A.dyn_frac = dyn_frac();
+    A.dyn_unit = dyn_unit();
+    if (k == 7 && variant == 22) {
+        int dev = 0;
+        if (grid > kClaimMaxGrid) return kf_fail(KF_EINVAL, "grid %d exceeds the claim buffer", grid);
+        if (hipGetDevice(&dev) != hipSuccess || !(A.claim = claim_buffer(dev, s)))
+            return kf_fail(KF_EHIP, "claim buffer allocation failed");
+    }
     if (hipLaunchKernel(count_kernel_for(k, variant), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (A.prof) {

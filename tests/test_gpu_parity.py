@@ -390,7 +390,7 @@ def test_arbitrary_byte_values(torch_dev, oracle, k):
     check_against_oracle(oracle, blobs, k, counts, totals, fmt=1, tag="bytes")
 
 
-@pytest.mark.parametrize("variant", [5, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("variant", [5, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
 def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, variant):
     """k=7 pair kernels (5: self-contained chunks, 10: static wave ranges, 12/13:
     32-byte lanes): their
@@ -419,7 +419,7 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, 
     check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16-many")
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
 def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
     """k=7 pair kernels (KF_COUNT_VARIANT 5, 6, 7: self-contained chunks, prefetch
     ring 6 / 4 / 8; 10, 11: static wave ranges, ring 6 / 8; 12, 13: 32-byte lanes,
@@ -433,7 +433,7 @@ def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
     check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"v{variant}")
 
 
-@pytest.mark.parametrize("variant", [20])
+@pytest.mark.parametrize("variant", [20, 22])
 def test_k7_many_pieces_many_records(torch_dev, oracle, monkeypatch, variant):
     """Several genome pieces per workgroup, each with many records (excluded
     intervals), N runs and empty genomes."""
@@ -443,3 +443,22 @@ def test_k7_many_pieces_many_records(torch_dev, oracle, monkeypatch, variant):
                               lower=0.05, crlf_rate=0.02, poly_rate=0.01) for i in range(700)]
     counts, totals = run_batch(blobs, 7, torch_dev)
     check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"pieces-v{variant}")
+
+
+@pytest.mark.parametrize("frac,unit", [("0", "1"), ("0.5", "3"), ("1", "2"), ("0.85", "2"), ("0.9", "64")])
+def test_k7_claimed_units(torch_dev, oracle, monkeypatch, frac, unit):
+    """Variant 22 (K1x whose waves claim the last part of each piece in units
+    from a per-workgroup ticket): every static/claimed split, unit sizes from one
+    3 KiB iteration to 64, low-complexity genomes whose u16 drains happen inside
+    claimed units, and repeated launches (the tickets continue across launches)."""
+    monkeypatch.setenv("KF_COUNT_VARIANT", "22")
+    monkeypatch.setenv("KF_DYN_FRAC", frac)
+    monkeypatch.setenv("KF_DYN_UNIT", unit)
+    rng = np.random.default_rng(777 + int(float(frac) * 100) + int(unit))
+    blobs = [gen.random_fasta(rng, int(rng.integers(0, 1_500_000)), max_records=4, n_rate=0.002, lower=0.05,
+                              crlf_rate=0.02, poly_rate=0.01) for _ in range(24)]
+    blobs.append(b">polyA\n" + gen.wrap(np.frombuffer(b"A" * 6_000_000, np.uint8), 80))
+    blobs.append(b">ac\n" + gen.wrap(np.frombuffer(b"AC" * 2_000_000, np.uint8), 61))
+    for rep in range(2):
+        counts, totals = run_batch(blobs, 7, torch_dev)
+        check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"claim-{frac}-{unit}-{rep}")

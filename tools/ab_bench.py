@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--n-period", type=int, default=0)
     ap.add_argument("--accumulate", action="store_true", help="zero outside the events, accumulate=True")
     ap.add_argument("--weights", default="", help="';'-separated KF_WAVE_WEIGHTS sets, alternated per round")
+    ap.add_argument("--env", default="", help="';'-separated sets of NAME=VAL[,NAME=VAL] (e.g. KF_DYN_FRAC=0.8), "
+                    "alternated per round like --weights")
     args = ap.parse_args()
     import torch
     from kf2vecfsw_amd import counter as C
@@ -35,13 +37,22 @@ def main():
     kc = C.KmerCounter(args.k, dev)
     fasta = int(db.off[-1].item())
     wsets = args.weights.split(";") if args.weights else [""]
+    if args.env:
+        wsets = args.env.split(";")
+    env_names = {kv.split("=")[0] for w in wsets for kv in w.split(",") if "=" in kv}
     variants = [(int(v), w) for v in args.variants.split(",") for w in wsets]
     times = {v: [] for v in variants}
     ref = None
     for r in range(args.rounds):
         for v, w in variants:
             os.environ["KF_COUNT_VARIANT"] = str(v)
-            if w:
+            if args.env:
+                for n in env_names:
+                    os.environ.pop(n, None)
+                for kv in w.split(","):
+                    if "=" in kv:
+                        os.environ[kv.split("=")[0]] = kv.split("=", 1)[1]
+            elif w:
                 os.environ["KF_WAVE_WEIGHTS"] = w
             else:
                 os.environ.pop("KF_WAVE_WEIGHTS", None)
