@@ -433,7 +433,7 @@ def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
     check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"v{variant}")
 
 
-@pytest.mark.parametrize("variant", [20, 22])
+@pytest.mark.parametrize("variant", [19, 20, 22])
 def test_k7_many_pieces_many_records(torch_dev, oracle, monkeypatch, variant):
     """Several genome pieces per workgroup, each with many records (excluded
     intervals), N runs and empty genomes."""
@@ -462,3 +462,59 @@ def test_k7_claimed_units(torch_dev, oracle, monkeypatch, frac, unit):
     for rep in range(2):
         counts, totals = run_batch(blobs, 7, torch_dev)
         check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"claim-{frac}-{unit}-{rep}")
+
+
+def _k1x_wave_ranges(total, grid, wts=(20, 17, 11, 6)):
+    """K1x's wave ranges for one genome at offset 0 of `total` bytes (count_kernel:
+    workgroup spans, then split_at_frac by wave_frac; kf_front.h)."""
+    def frac(w):
+        if w == 0:
+            return 0
+        if w >= 16:
+            return 1 << 20
+        s, r = w >> 2, w & 3
+        return ((sum(4 * wts[i] for i in range(s)) + r * wts[s]) << 20) // (4 * sum(wts))
+
+    def split(plo, phi, fr):
+        if fr >= 1 << 20:
+            return phi
+        return min(max((plo + (((phi - plo) * fr) >> 20)) & ~15, plo), phi)
+
+    out = []
+    for b in range(grid):
+        lo = (total // grid * b + (total % grid) * b // grid) & ~15
+        hi = total if b + 1 == grid else (total // grid * (b + 1) + (total % grid) * (b + 1) // grid) & ~15
+        out += [(split(lo, hi, frac(w)), split(lo, hi, frac(w + 1))) for w in range(16)]
+    return out
+
+
+@pytest.mark.parametrize("variant", [18, 19, 21, 22, pytest.param(20, marks=pytest.mark.xfail(
+    reason="variant 20 checks returns every other iteration: a counter grown only in unchecked iterations "
+           "passes 0xFFFF (why 19 is the default)", strict=True))])
+def test_k7_unchecked_iterations_adversarial(torch_dev, oracle, monkeypatch, variant):
+    """An input built against K1x's alternating return checks (variant 20: the
+    adds of every other 3 KiB iteration are not checked): every wave's odd
+    (unchecked) iterations are poly-A and its even ones hold no A at all, so no
+    checked add ever sees the AAAAAAAA counter, which alone would pass 0xFFFF
+    within one workgroup's piece.  The counts must still be exact."""
+    monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
+    monkeypatch.delenv("KF_WAVE_WEIGHTS", raising=False)
+    rng = np.random.default_rng(99)
+    L = 80_000_000
+    head = b">adv\n"
+    arr = np.frombuffer(b"CGT", np.uint8)[rng.integers(0, 3, L)].copy()
+    arr[: len(head)] = np.frombuffer(head, np.uint8)
+    grid = counter(7, torch_dev).launch_info()[0]
+    total = (L + 15) // 16 * 16
+    for lo, hi in _k1x_wave_ranges(total, grid):
+        c0 = lo & ~15
+        i = 1
+        while c0 + 3072 * (i + 1) <= hi:
+            arr[c0 + 3072 * i: c0 + 3072 * (i + 1)] = ord("A")
+            i += 2
+    arr[: len(head)] = np.frombuffer(head, np.uint8)
+    pos = np.arange(len(head), L)
+    arr[pos[(pos - len(head)) % 81 == 80]] = 10
+    blobs = [arr.tobytes()]
+    counts, totals = run_batch(blobs, 7, torch_dev)
+    check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"adv-v{variant}")

@@ -4,7 +4,7 @@
 set -u
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 ROUND=${ROUND:-r02}
-V7=${V7:-20}   # the k=7 default variant (KF_COUNT_VARIANT)
+V7=${V7:-19}   # the k=7 default variant (KF_COUNT_VARIANT)
 for k in 7 11; do
   if [ $k -le 8 ]; then KN="count_kernel<$k, $V7>"; else KN="bucket_kernel<$k>"; fi
   PMC_TAG=pmc_k$k VARIANT=$V7 GROUPS_LIST=$'FETCH_SIZE\nWRITE_SIZE' AB_ARGS="--k $k" bash "$REPO/tools/pmc_variant.sh" || exit $?
