@@ -224,6 +224,17 @@ def get_frequencies(args) -> None:
     reader = ThreadPoolExecutor(max_workers=depth)
     writer = ThreadPoolExecutor(max_workers=1)
     reads = deque(reader.submit(pack, batches[i]) for i in range(min(depth, len(batches))))
+    # While the first batches are read: the side stream's first event and launch
+    # and the device block for a batch (the caching allocator keeps it for this
+    # stream) would otherwise cost ~2 ms between the first read and its H2D
+    # (KF_TRACE: got 0 -> issue 0, tools/e2e_bench.py).
+    big = max(sum((os.path.getsize(paths[i]) + 15) // 16 * 16 for i in b) for b in batches)
+    with torch.cuda.stream(stream):
+        warm = torch.empty(big + 16, dtype=torch.uint8, device=device)
+        warm[:16].zero_()
+        torch.cuda.Event(enable_timing=True).record(stream)
+        del warm
+    stream.synchronize()
     writes = []
     # batches whose .kf files may still be waiting for the writer: each holds a
     # pinned count matrix (4 x bins B per genome), so the backlog is bounded
