@@ -55,7 +55,11 @@ namespace kf {
 //             genome piece statically and claim the rest in small units from a
 //             per-workgroup ticket (KF_DYN_FRAC, KF_DYN_UNIT), so they finish a
 //             piece together
-constexpr int kNumVariants = 23;
+//   variant 23: K1x variant 19 whose waves claim their own range's 3 KiB
+//             iterations one by one from the front (with the loads, two ahead)
+//             while waves that are done take the back half of the range with
+//             the most left (compare-and-swap on the range's word)
+constexpr int kNumVariants = 24;
 constexpr int kDefaultVariant = 19;   // K1x (every add's return checked, ring 2) at k = 7; variant 1 (K1) for every other k
 // (variant 20, returns checked every other iteration, is not exact on inputs built so that
 // a counter only grows in unchecked iterations: test_k7_unchecked_iterations_adversarial)
@@ -98,7 +102,8 @@ template <> struct Shape<19> { static constexpr int block = 1024, wpe = 4, abl =
 template <> struct Shape<20> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // + alternating checks
 template <> struct Shape<21> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // + paired iterations
 template <> struct Shape<22> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // 19 + claimed tail units
-template <int V> constexpr bool kX = V >= 18 && V <= 22;
+template <> struct Shape<23> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // 19 + stealing
+template <int V> constexpr bool kX = V >= 18 && V <= 23;
 template <int V> constexpr bool kStaticPair = V == 10 || V == 11 || kWide<V> || kX<V>;
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
@@ -1236,7 +1241,8 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
 template <int RING, bool ALT = false, bool PAIRED = false>
 __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                     uint64_t lo, uint64_t hi, int lane, uint32_t& drained,
-                                                    uint32_t piece = 0, IvHint* hint = nullptr) {
+                                                    uint32_t piece = 0, IvHint* hint = nullptr,
+                                                    unsigned long long* own = nullptr, uint32_t tag = 0) {
     static_assert(!ALT || RING == 2, "alternating checks need a 2-slot ring");
     static_assert(!PAIRED || (RING == 2 && !ALT), "paired iterations need a 2-slot ring");
     constexpr uint32_t HOT = (ALT || PAIRED) ? kXHot : kWideHot, STEP = (ALT || PAIRED) ? kXStep : kWideStep;
@@ -1248,6 +1254,26 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
     XBlock buf[RING];
 #pragma unroll
     for (int j = 0; j < RING; ++j) buf[j] = x_load(A.bytes, rg.c0, j * kXChunk, rg.end_r, lane);
+    const uint32_t nx = (rg.nch + 2) / 3;   // 3 KiB iterations
+    // variant 23: the range's iterations are claimed one by one from its word
+    // (tag << 48 | back << 24 | front), RING iterations ahead with the loads, so
+    // other waves can take iterations from the back (claim_steal)
+    unsigned long long cl[RING];
+    if (own) {
+        if (lane == 0) {
+            __hip_atomic_store(own, ((unsigned long long)tag << 48) | ((unsigned long long)nx << 24), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int j = 0; j < RING; ++j)
+                cl[j] = __hip_atomic_fetch_add(own, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // iteration `it` is this wave's if the claim made for it saw back > it
+    auto owned = [&](int j, uint32_t it) -> bool {
+        const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(cl[j] >> 32));
+        const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cl[j]);
+        return it < (((h & 0xFFFFu) << 8) | (l >> 24));
+    };
     rg.warm16<7>(A, lane, hint);
     // the cursor as it stands at the range start (the loop's tests of a last
     // iteration's thirds may advance it past intervals beyond the range end)
@@ -1317,7 +1343,7 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         }
         rel += kXChunk;
     };
-    const uint32_t nx = (rg.nch + 2) / 3;   // 3 KiB iterations
+    bool stop = false;
     for (uint32_t i = 0; i + RING <= nx; i += RING) {
         if constexpr (PAIRED) {
             if (!rg.masked_span(A, rel, 2 * kXChunk)) {
@@ -1340,18 +1366,27 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         }
 #pragma unroll
         for (int j = 0; j < RING; ++j) {
+            if (own && !owned(j, i + j)) {
+                stop = true;
+                break;
+            }
             step(buf[j], j);
 #if KF_K1W_ABL == 5   // profiling only: every iteration re-reads the range's first chunks (cache hits)
             buf[j] = x_load(A.bytes, rg.c0, (uint32_t)j * kXChunk, rg.end_r, lane);
 #else
             buf[j] = x_load(A.bytes, rg.c0, rel + (RING - 1) * kXChunk, rg.end_r, lane);
 #endif
+            if (own && lane == 0) cl[j] = __hip_atomic_fetch_add(own, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        if (stop) break;
     }
     const uint32_t rem = nx % RING;
 #pragma unroll
     for (int j = 0; j < RING - 1; ++j)
-        if (rem > (uint32_t)j) step(buf[j], j);
+        if (!stop && rem > (uint32_t)j) {
+            if (own && !owned(j, nx - rem + j)) break;
+            step(buf[j], j);
+        }
     if (A.prof && lane == 0) {   // KF_COUNT_PROFILE=1: per-wave-slot loop cycles per 1 KiB chunk
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         const uint64_t t_end = __builtin_amdgcn_s_memtime();
@@ -1543,8 +1578,54 @@ __global__ void __launch_bounds__(Shape<V>::block)
                     if (V == 22 && claimed && lane == 0)
                         t_next = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     s += process_range_x<Shape<V>::ring, V == 20, V == 21>(
-                        A, g, glo, ghi, rlo, rhi, lane, drained, npiece, V == 22 ? &hint : nullptr);
-                    if constexpr (V != 22) break;
+                        A, g, glo, ghi, rlo, rhi, lane, drained, npiece, V == 22 ? &hint : nullptr,
+                        V == 23 && !claimed ? (unsigned long long*)tk + wave : nullptr, (npiece + 1u) & 0xFFFFu);
+                    if constexpr (V != 22 && V != 23) break;
+                    if constexpr (V == 23) {
+                        // variant 23: take the back half of the range with the most
+                        // iterations left (its owner claims from the front)
+                        claimed = true;
+                        const uint32_t tag = (npiece + 1u) & 0xFFFFu;
+                        unsigned long long* const words = (unsigned long long*)tk;
+                        unsigned long long w = 0;
+                        if (lane < kWaves) w = __hip_atomic_load(words + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint32_t f = (uint32_t)w & 0xFFFFFFu, bk = (uint32_t)(w >> 24) & 0xFFFFFFu;
+                        const uint32_t left = ((uint32_t)(w >> 48) == tag && bk > f) ? bk - f : 0u;
+                        uint32_t key = lane < kWaves ? (min(left, 0x3FFFFFu) << 5) | (uint32_t)lane : 0u;
+#pragma unroll
+                        for (int d = 1; d < kWaves; d <<= 1) key = max(key, (uint32_t)__shfl_xor((int)key, d, kWave));
+                        key = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
+                        if ((key >> 5) < 2u) break;
+                        const uint32_t v = key & 31u;
+                        uint32_t a = 0, b = 0;
+                        if (lane == 0) {
+                            unsigned long long cur = __hip_atomic_load(words + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            for (;;) {
+                                const uint32_t cf = (uint32_t)cur & 0xFFFFFFu, cb = (uint32_t)(cur >> 24) & 0xFFFFFFu;
+                                if ((uint32_t)(cur >> 48) != tag || cb < cf + 2u) break;
+                                const uint32_t kk = (cb - cf) / 2u;
+                                if (__hip_atomic_compare_exchange_strong(words + v, &cur, cur - ((unsigned long long)kk << 24),
+                                                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+                                    a = cb - kk, b = cb;
+                                    break;
+                                }
+                            }
+                        }
+                        a = (uint32_t)__builtin_amdgcn_readfirstlane((int)a);
+                        b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+                        if (a < b) {   // the victim's range, iterations [a, b)
+                            const uint64_t vlo = split_at_frac(plo, dlo, wave_frac(v, A.wave_w));
+                            const uint64_t vhi = split_at_frac(plo, dlo, wave_frac(v + 1, A.wave_w));
+                            const uint64_t vc0 = vlo & ~(uint64_t)15;
+                            rlo = max(vlo, vc0 + (uint64_t)a * kXChunk);
+                            rhi = min(vhi, vc0 + (uint64_t)b * kXChunk);
+                        } else {
+                            rlo = rhi = 0;   // lost the race: look again
+                        }
+                        __builtin_amdgcn_s_setprio(3);
+                        continue;
+                    }
                     if (!claimed && lane == 0)
                         t_next = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     claimed = true;
@@ -2239,7 +2320,7 @@ void* count_kernel_v(int k) {
 // Variants >= kFirstPairVariant are the pair kernel at k = 7 and variant 1 elsewhere.
 bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant && v <= 7; }
 bool is_dyn(int k, int v) { return k <= kLdsMaxK && (v == 8 || v == 9); }
-bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 22; }
+bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 23; }
 int effective_variant(int k, int v) {
     return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v) && !is_static_pair(k, v)) ? 1 : v;
 }
@@ -2278,6 +2359,7 @@ void* count_kernel_for(int k, int v) {
         case 20: return (void*)&count_kernel<7, 20>;
         case 21: return (void*)&count_kernel<7, 21>;
         case 22: return (void*)&count_kernel<7, 22>;
+        case 23: return (void*)&count_kernel<7, 23>;
         default: return (void*)&count_kernel<7, 10>;
         }
     }
@@ -2466,7 +2548,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     A.claim = nullptr;
     A.dyn_frac = dyn_frac();
     A.dyn_unit = dyn_unit();
-    if (k == 7 && variant == 22) {
+    if (k == 7 && (variant == 22 || variant == 23)) {
         int dev = 0;
         if (grid > kClaimMaxGrid) return kf_fail(KF_EINVAL, "grid %d exceeds the claim buffer", grid);
         if (hipGetDevice(&dev) != hipSuccess || !(A.claim = claim_buffer(dev, s)))

@@ -390,7 +390,7 @@ def test_arbitrary_byte_values(torch_dev, oracle, k):
     check_against_oracle(oracle, blobs, k, counts, totals, fmt=1, tag="bytes")
 
 
-@pytest.mark.parametrize("variant", [5, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
+@pytest.mark.parametrize("variant", [5, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23])
 def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, variant):
     """k=7 pair kernels (5: self-contained chunks, 10: static wave ranges, 12/13:
     32-byte lanes): their
@@ -419,7 +419,7 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, 
     check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16-many")
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
+@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23])
 def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
     """k=7 pair kernels (KF_COUNT_VARIANT 5, 6, 7: self-contained chunks, prefetch
     ring 6 / 4 / 8; 10, 11: static wave ranges, ring 6 / 8; 12, 13: 32-byte lanes,
@@ -433,7 +433,7 @@ def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
     check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"v{variant}")
 
 
-@pytest.mark.parametrize("variant", [19, 20, 22])
+@pytest.mark.parametrize("variant", [19, 20, 22, 23])
 def test_k7_many_pieces_many_records(torch_dev, oracle, monkeypatch, variant):
     """Several genome pieces per workgroup, each with many records (excluded
     intervals), N runs and empty genomes."""
@@ -488,7 +488,7 @@ def _k1x_wave_ranges(total, grid, wts=(20, 17, 11, 6)):
     return out
 
 
-@pytest.mark.parametrize("variant", [18, 19, 21, 22, pytest.param(20, marks=pytest.mark.xfail(
+@pytest.mark.parametrize("variant", [18, 19, 21, 22, 23, pytest.param(20, marks=pytest.mark.xfail(
     reason="variant 20 checks returns every other iteration: a counter grown only in unchecked iterations "
            "passes 0xFFFF (why 19 is the default)", strict=True))])
 def test_k7_unchecked_iterations_adversarial(torch_dev, oracle, monkeypatch, variant):
@@ -518,3 +518,17 @@ def test_k7_unchecked_iterations_adversarial(torch_dev, oracle, monkeypatch, var
     blobs = [arr.tobytes()]
     counts, totals = run_batch(blobs, 7, torch_dev)
     check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"adv-v{variant}")
+
+
+def test_k7_stealing_repeated_launches(torch_dev, oracle, monkeypatch):
+    """Variant 23 (waves claim their own iterations from the front while idle
+    waves take back halves): genomes of every size class in one batch, several
+    launches in a row (the range words persist between launches, tagged by piece)."""
+    monkeypatch.setenv("KF_COUNT_VARIANT", "23")
+    rng = np.random.default_rng(2323)
+    blobs = [gen.random_fasta(rng, int(rng.choice([0, 100, 5000, 300_000, 3_000_000])), max_records=6, n_rate=0.002,
+                              lower=0.05, crlf_rate=0.01, poly_rate=0.01) for _ in range(40)]
+    blobs.append(b">polyA\n" + gen.wrap(np.frombuffer(b"A" * 8_000_000, np.uint8), 80))
+    for rep in range(3):
+        counts, totals = run_batch(blobs, 7, torch_dev)
+        check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"steal-{rep}")
