@@ -59,10 +59,14 @@ namespace kf {
 //             iterations one by one from the front (with the loads, two ahead)
 //             while waves that are done take the back half of the range with
 //             the most left (compare-and-swap on the range's word)
-constexpr int kNumVariants = 24;
+//   variant 24: k = 8 on the K1x front end (48-byte lanes): every window an
+//             8-mer in 65,536 u16 LDS counters, one pass (instead of K2's two);
+//             for every other k it runs as variant 1
+constexpr int kNumVariants = 25;
 constexpr int kDefaultVariant = 19;   // K1x (every add's return checked, ring 2) at k = 7; variant 1 (K1) for every other k
 // (variant 20, returns checked every other iteration, is not exact on inputs built so that
 // a counter only grows in unchecked iterations: test_k7_unchecked_iterations_adversarial)
+constexpr int kDefaultVariantK8 = 24;   // k = 8: single pass on the K1x front end (K2, variant 1, takes two)
 constexpr int kFirstPairVariant = 5;
 // K1x default shares by wave age slot (KF_WAVE_WEIGHTS overrides)
 constexpr uint32_t kWaveW0 = 20, kWaveW1 = 17, kWaveW2 = 11, kWaveW3 = 6;
@@ -103,7 +107,8 @@ template <> struct Shape<20> { static constexpr int block = 1024, wpe = 4, abl =
 template <> struct Shape<21> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // + paired iterations
 template <> struct Shape<22> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // 19 + claimed tail units
 template <> struct Shape<23> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // 19 + stealing
-template <int V> constexpr bool kX = V >= 18 && V <= 23;
+template <> struct Shape<24> { static constexpr int block = 1024, wpe = 4, abl = 0, ring = 2; };   // k = 8 on K1x
+template <int V> constexpr bool kX = V >= 18 && V <= 24;
 template <int V> constexpr bool kStaticPair = V == 10 || V == 11 || kWide<V> || kX<V>;
 #ifdef KF_ABLATION
 // profiling-only builds (python -m kf2vecfsw_amd.build --ablation): wrong counts by design
@@ -727,7 +732,8 @@ constexpr uint32_t kWideStep = 0x4000u;
 // below STEP (compare-and-swap: exact under concurrent adds).  P word: 8-mers 2w,
 // 2w+1; S word (a >= kPairSBase): forward 7-mers 2w, 2w+1.  K1w: STEP 0x4000;
 // K1x: 0x2000 (it checks returns every other iteration, see x_fast).
-template <uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
+// K = 8 (variant 24): a P half is one 8-mer, whose column is code2col[bin].
+template <uint32_t HOT = kWideHot, uint32_t STEP = kWideStep, int K = 7>
 __device__ __noinline__ void wide_drain(uint32_t a, const uint32_t* __restrict__ code2col, uint32_t* gcounts) {
     lds_u32* p = (lds_u32*)(uintptr_t)a;
     uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -741,7 +747,9 @@ __device__ __noinline__ void wide_drain(uint32_t a, const uint32_t* __restrict__
             for (uint32_t h = 0; h < 2; ++h) {
                 if (!((sub >> (16 * h)) & 0xFFFFu)) continue;
                 const uint32_t bin = 2 * w + h;
-                if (single) {
+                if (K == 8) {
+                    atomicAdd(gcounts + code2col[bin], STEP);
+                } else if (single) {
                     atomicAdd(gcounts + code2col[bin], STEP);
                 } else {
                     atomicAdd(gcounts + code2col[bin >> 2], STEP);       // older 7-mer
@@ -754,12 +762,12 @@ __device__ __noinline__ void wide_drain(uint32_t a, const uint32_t* __restrict__
         }
     }
 }
-template <uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
+template <uint32_t HOT = kWideHot, uint32_t STEP = kWideStep, int K = 7>
 __device__ __noinline__ void wide_scan_drain(const uint32_t* __restrict__ code2col, uint32_t* gcounts, int lane) {
-    for (uint32_t w = (uint32_t)lane; w < kFwdSEnd / 4; w += kWave) {
+    for (uint32_t w = (uint32_t)lane; w < (K == 8 ? kPairSBase : kFwdSEnd) / 4; w += kWave) {
         const uint32_t v = __hip_atomic_load((lds_u32*)(uintptr_t)(4 * w), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (v & HOT) wide_drain<HOT, STEP>(4 * w, code2col, gcounts);
+        if (v & HOT) wide_drain<HOT, STEP, K>(4 * w, code2col, gcounts);
     }
 }
 constexpr uint32_t kXHot = 0xE000E000u;   // K1x: a half >= 0x2000
@@ -898,11 +906,11 @@ __device__ __forceinline__ bool wide_fast(const WideBlock& d, const CountArgs& A
 
 // Irregular 1 KiB chunk (16-byte lane layout, count_chunk's general path): every
 // counted window as a single into S by its forward code; returns checked at once.
-template <bool MASKED, uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
+// K = 8 (variant 24): every window is an 8-mer counted in P (u16 half of word y >> 1).
+template <bool MASKED, uint32_t HOT = kWideHot, uint32_t STEP = kWideStep, int K = 7>
 __device__ __forceinline__ uint32_t wide_singles(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
                                                  const ChunkMask& m, uint64_t iv0, uint32_t carry, uint32_t* gcounts,
                                                  uint32_t& lane_total, uint32_t& drained) {
-    constexpr int K = 7;
     uint32_t C, V, EN, ne, own;
     front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
     const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
@@ -914,10 +922,10 @@ __device__ __forceinline__ uint32_t wide_singles(const uint4 d, const CountArgs&
     for (int r = 0; r < 16; ++r) {
         const int fo = (2 * r) & ~7;
         const uint32_t y = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, 2 * K);
-        o |= lds_add_rtn(kPairSBase + ((y >> 1) << 2), ((R >> r) & 1u) * half_one(y));
+        o |= lds_add_rtn((K == 8 ? 0u : kPairSBase) + ((y >> 1) << 2), ((R >> r) & 1u) * half_one(y));
     }
     if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
-        wide_scan_drain<HOT, STEP>(A.code2col, gcounts, lane);
+        wide_scan_drain<HOT, STEP, K>(A.code2col, gcounts, lane);
         drained = 1;
     }
     lane_total += (uint32_t)__builtin_popcount(R);
@@ -1198,13 +1206,83 @@ __device__ __forceinline__ uint32_t x_body(const XCls& k, uint32_t& carry, uint3
     return o;
 }
 
-template <bool CHECK = true, uint32_t HOT = kWideHot, uint32_t STEP = kWideStep>
+// k = 8 (variant 24): the counting half of a fast iteration with every window
+// an 8-mer in P (65,536 u16 counters, half y & 1 of word y >> 1): window r =
+// bits [2r, 2r + 16) of W, address (X >> 2r) & 0x1FFFC with X = W << 1, half =
+// W bit 2r.  48 adds per lane (47 with a newline: window 47 then adds 0).
+// Every return is checked (HOT = 0x2000 per half: a half stays below 0x2000 +
+// 16 x 48 x 64 = 0xE000).
+template <bool CHECK>
+__device__ __forceinline__ uint32_t x_body8(const XCls& k, uint32_t& carry, uint32_t& lane_total) {
+    constexpr uint32_t TM = (1u << 14) - 1u;   // 7 context entries
+    const uint32_t V = k.V;
+    const uint32_t C[3] = {k.C[0], k.C[1], k.C[2]};
+    uint32_t nl;
+    asm("v_min_u32_e32 %0, 1, %1" : "=v"(nl) : "v"(V));
+    const uint32_t e2 = V - 98u;
+    const uint32_t q0 = min(e2, 32u), q1 = min(max(e2, 32u), 64u) - 32u, q2 = min(max(e2, 64u) - 64u, 32u);
+    const uint32_t L0 = (uint32_t)(~0ull << q0), L1 = (uint32_t)(~0ull << q1), L2 = (uint32_t)(~0ull << q2);
+    const uint32_t c0 = bfi(L0, __builtin_amdgcn_alignbit(C[1], C[0], 2), C[0]);
+    const uint32_t c1 = bfi(L1, __builtin_amdgcn_alignbit(C[2], C[1], 2), C[1]);
+    const uint32_t c2 = bfi(L2, C[2] >> 2, C[2]);
+    const uint32_t pC = wave_shr1(t_codes(carry), c0);
+    const uint64_t t = (uint64_t)pC << (32u - 2u * nl);
+    const uint32_t w0 = c0, w1 = c1, w2 = c2 | (uint32_t)t, w3 = (uint32_t)(t >> 32);
+    const uint32_t x0 = w0 << 1, x1 = __builtin_amdgcn_alignbit(w1, w0, 31), x2 = __builtin_amdgcn_alignbit(w2, w1, 31),
+                   x3 = __builtin_amdgcn_alignbit(w3, w2, 31);
+    const uint32_t X[3] = {x0, x1, x2};
+    const uint32_t Y[3] = {__builtin_amdgcn_alignbit(x1, x0, 16), __builtin_amdgcn_alignbit(x2, x1, 16),
+                           __builtin_amdgcn_alignbit(x3, x2, 16)};
+    const uint32_t Wd[3] = {w0, w1, w2};
+    constexpr uint32_t PM = 0x1FFFCu;
+    const uint32_t one = 1u;
+    const uint32_t keep47 = nl - 1u;   // 0 with a newline: window 47 is lane L-1's window 0
+    uint32_t o = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint32_t rt[24];
+#pragma unroll
+        for (int q = 0; q < 24; ++q) {
+            const int r = 24 * h + q, i = r >> 4, tt = r & 15;
+            const uint32_t a = ((tt < 8 ? X[i] : Y[i]) >> (2 * (tt & 7))) & PM;
+            const int tb = tt & 3;   // W bit 2r sits at bit 8m + 2tb of Wd[i] (m = tt >> 2): move it to 8m + 4
+            const uint32_t H = (tb == 0 ? Wd[i] << 4 : (tb == 1 ? Wd[i] << 2 : (tb == 2 ? Wd[i] : Wd[i] >> 2))) & 0x10101010u;
+            uint32_t dl;
+            switch (tt >> 2) {
+            case 0: dl = shl1_byte<0>(H, one); break;
+            case 1: dl = shl1_byte<1>(H, one); break;
+            case 2: dl = shl1_byte<2>(H, one); break;
+            default: dl = shl1_byte<3>(H, one); break;
+            }
+            if (r == 47) dl &= keep47;
+            if constexpr (CHECK) {
+                rt[q] = lds_add_rtn(a, dl);
+            } else {
+                lds_add(a, dl);
+                rt[q] = 0;
+            }
+        }
+        if constexpr (CHECK) {
+#pragma unroll
+            for (int q = 0; q < 24; q += 3) o |= rt[q] | rt[q + 1] | rt[q + 2];
+        }
+    }
+    lane_total -= nl;
+    carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)c0, kWave - 1) & TM, 31u, 31u);
+    return o;
+}
+
+template <bool CHECK = true, uint32_t HOT = kWideHot, uint32_t STEP = kWideStep, int K = 7>
 __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
                                        uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
     const XCls k = x_cls(d);
     carry = __builtin_amdgcn_readfirstlane(carry);   // wave-uniform: its tests run on the SALU
-    if (t_n(carry) < 6u || __builtin_amdgcn_ballot_w64(k.V >= 196u) != 0) return false;
-    const uint32_t o = x_body<CHECK>(k, carry, lane_total);
+    if (t_n(carry) < (uint32_t)(K - 1) || __builtin_amdgcn_ballot_w64(k.V >= 196u) != 0) return false;
+    uint32_t o;
+    if constexpr (K == 8)
+        o = x_body8<CHECK>(k, carry, lane_total);
+    else
+        o = x_body<CHECK>(k, carry, lane_total);
 #ifdef KF_K1X_PAD   // profiling only: N extra VALU ops of one kind (1 = v_xor VOP2, 2 = v_perm VOP3)
     {
         const uint32_t w[12] = {d.q[0].x, d.q[0].y, d.q[0].z, d.q[0].w, d.q[1].x, d.q[1].y,
@@ -1222,7 +1300,7 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
     }
 #endif
     if (CHECK && __builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
-        wide_scan_drain<HOT, STEP>(A.code2col, gcounts, lane);
+        wide_scan_drain<HOT, STEP, K>(A.code2col, gcounts, lane);
         drained = 1;
     }
     return true;
@@ -1238,14 +1316,16 @@ __device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int 
 // u16 test of all 48 returns, threshold 0x2000), else one at a time.  Every add's
 // return is tested, at most two iterations after the add, so a half stays below
 // 0x2000 + 16 x 2 x 1536 = 0xE000.
-template <int RING, bool ALT = false, bool PAIRED = false>
+template <int RING, bool ALT = false, bool PAIRED = false, int K = 7>
 __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi,
                                                     uint64_t lo, uint64_t hi, int lane, uint32_t& drained,
                                                     uint32_t piece = 0, IvHint* hint = nullptr,
                                                     unsigned long long* own = nullptr, uint32_t tag = 0) {
     static_assert(!ALT || RING == 2, "alternating checks need a 2-slot ring");
     static_assert(!PAIRED || (RING == 2 && !ALT), "paired iterations need a 2-slot ring");
-    constexpr uint32_t HOT = (ALT || PAIRED) ? kXHot : kWideHot, STEP = (ALT || PAIRED) ? kXStep : kWideStep;
+    static_assert(K == 7 || (K == 8 && !ALT && !PAIRED), "k = 8 checks every return");
+    constexpr uint32_t HOT = (ALT || PAIRED || K == 8) ? kXHot : kWideHot;
+    constexpr uint32_t STEP = (ALT || PAIRED || K == 8) ? kXStep : kWideStep;
     if (lo >= hi) return 0;
     uint32_t* gcounts = A.counts + (uint64_t)g * A.nbins;
     const uint64_t t_begin = A.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -1274,7 +1354,7 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
         const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cl[j]);
         return it < (((h & 0xFFFFu) << 8) | (l >> 24));
     };
-    rg.warm16<7>(A, lane, hint);
+    rg.warm16<K>(A, lane, hint);
     // the cursor as it stands at the range start (the loop's tests of a last
     // iteration's thirds may advance it past intervals beyond the range end)
     if (hint) *hint = rg.hint();
@@ -1315,9 +1395,9 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
 #else
             if (!ALT || slot == 0)
 #endif
-                fast = x_fast<true, HOT, STEP>(bf, A, lane, carry, gcounts, lane_total, drained);
+                fast = x_fast<true, HOT, STEP, K>(bf, A, lane, carry, gcounts, lane_total, drained);
             else
-                fast = x_fast<false, HOT, STEP>(bf, A, lane, carry, gcounts, lane_total, drained);
+                fast = x_fast<false, HOT, STEP, K>(bf, A, lane, carry, gcounts, lane_total, drained);
         }
         nfast += fast ? 1u : 0u;
         if (!fast) {
@@ -1336,9 +1416,11 @@ __device__ __forceinline__ uint64_t process_range_x(const CountArgs& A, int32_t 
                 const uint64_t ivh = h == 0 ? iv0 : (h == 1 ? iv1 : rg.iv);
                 const uint4 hb = rg.load(A.bytes, r, lane);
                 if (mh)
-                    carry = wide_singles<true, HOT, STEP>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
+                    carry = wide_singles<true, HOT, STEP, K>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total,
+                                                             drained);
                 else
-                    carry = wide_singles<false, HOT, STEP>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
+                    carry = wide_singles<false, HOT, STEP, K>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total,
+                                                              drained);
             }
         }
         rel += kXChunk;
@@ -1491,7 +1573,8 @@ __global__ void __launch_bounds__(Shape<V>::block)
     constexpr bool GLOBAL = ModeOf<K>::mode == kModeGlobal;
     constexpr bool MULTI = ModeOf<K>::mode == kModeMulti;
     constexpr bool PAIR = kStaticPair<V>;
-    static_assert(!PAIR || (K == 7 && kBlock == 1024), "static pair counting is k = 7, 1024 threads");
+    static_assert(!PAIR || ((K == 7 || (K == 8 && V == 24)) && kBlock == 1024),
+                  "static pair counting is k = 7 (k = 8: variant 24), 1024 threads");
     // dynamic LDS: the histogram (PAIR: P and S) at offset 0 (so bin addresses need
     // no base add), then kWaves u64 reduction slots; no static __shared__ (it would
     // precede it)
@@ -1577,7 +1660,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
                 for (;;) {
                     if (V == 22 && claimed && lane == 0)
                         t_next = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    s += process_range_x<Shape<V>::ring, V == 20, V == 21>(
+                    s += process_range_x<Shape<V>::ring, V == 20, V == 21, (V == 24 ? 8 : 7)>(
                         A, g, glo, ghi, rlo, rhi, lane, drained, npiece, V == 22 ? &hint : nullptr,
                         V == 23 && !claimed ? (unsigned long long*)tk + wave : nullptr, (npiece + 1u) & 0xFFFFu);
                     if constexpr (V != 22 && V != 23) break;
@@ -1643,6 +1726,32 @@ __global__ void __launch_bounds__(Shape<V>::block)
             if constexpr (!kX<V> && !kWide<V>)
                 s = process_range<K, false, 0, Shape<V>::ring, true>(A, g, glo, ghi, lo_c, hi_c, lane, hist, 0);
             const uint64_t t_p0 = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+            if constexpr (K == 8) {
+                // variant 24 flush: canonical 8-mer column = P[rep] + P[rc rep]
+                // (a palindrome once); drain flags in the unused S area
+                (void)t_p0;
+                lds_barrier();   // every add of this piece is done
+                if (lane == 0) hist[kPairSBase / 4 + wave] = drained;
+                lds_barrier();
+                const uint4* fl = (const uint4*)(hist + kPairSBase / 4);
+                const uint4 f0 = fl[0], f1 = fl[1], f2 = fl[2], f3 = fl[3];
+                const bool any_drain = (f0.x | f0.y | f0.z | f0.w | f1.x | f1.y | f1.z | f1.w | f2.x | f2.y | f2.z |
+                                        f2.w | f3.x | f3.y | f3.z | f3.w) != 0;
+                const bool whole = plo == glo && phi == ghi && !(A.flags & KF_ACCUMULATE);
+                for (uint32_t col = tid; col < A.nbins; col += kBlock) {
+                    const uint32_t y = A.col2rep[col], rc = kf_revcomp<8>(y);
+                    uint32_t v = (hist[y >> 1] >> ((y & 1u) << 4)) & 0xFFFFu;
+                    if (rc != y) v += (hist[rc >> 1] >> ((rc & 1u) << 4)) & 0xFFFFu;
+                    if (whole && !any_drain)
+                        gc[col] = v;   // this workgroup owns row g (zeroed by the caller)
+                    else if (v)
+                        __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                lds_barrier();   // columns read
+                uint4* h4 = (uint4*)hist;
+                for (uint32_t i = tid; i < kFwdSEnd / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+                ++npiece;
+            } else {
             // the columns' forward representatives, loaded before the barrier so
             // their latency overlaps it.  A whole genome (the common case) takes
             // four consecutive columns per lane and 16-byte row stores (the flush
@@ -1725,6 +1834,7 @@ __global__ void __launch_bounds__(Shape<V>::block)
                 atomicAdd(A.prof + 4, 1ull);
                 atomicAdd(A.prof + 5, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_p1));
             }
+            }   // (K == 7)
         }
         for (uint32_t pass = 0; pass < (PAIR ? 0u : (uint32_t)ModeOf<K>::passes); ++pass) {
             const uint64_t lt = process_range<K, GLOBAL, Shape<V>::abl, Shape<V>::ring>(A, g, glo, ghi, lo_c, hi_c, lane, hist, pass);
@@ -2331,8 +2441,10 @@ void* count_kernel_v(int k) {
 bool is_pair(int k, int v) { return k == 7 && v >= kFirstPairVariant && v <= 7; }
 bool is_dyn(int k, int v) { return k <= kLdsMaxK && (v == 8 || v == 9); }
 bool is_static_pair(int k, int v) { return k == 7 && v >= 10 && v <= 23; }
+bool is_k8x(int k, int v) { return k == 8 && v == 24; }
 int effective_variant(int k, int v) {
-    return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v) && !is_static_pair(k, v)) ? 1 : v;
+    return (v >= kFirstPairVariant && !is_pair(k, v) && !is_dyn(k, v) && !is_static_pair(k, v) && !is_k8x(k, v)) ? 1
+                                                                                                                : v;
 }
 
 template <int V>
@@ -2355,6 +2467,7 @@ void* count_kernel_for(int k, int v) {
         return (void*)&pair_kernel<5>;
     }
     if (is_dyn(k, v)) return v == 9 ? dyn_kernel_v<9>(k) : dyn_kernel_v<8>(k);
+    if (is_k8x(k, v)) return (void*)&count_kernel<8, 24>;
     if (is_static_pair(k, v)) {
         switch (v) {
         case 11: return (void*)&count_kernel<7, 11>;
@@ -2394,11 +2507,14 @@ int bucket_min_k() {
 }
 
 // KF_COUNT_VARIANT (tuning/A-B knob, read per launch): workgroup shape, see Shape<>.
-int current_variant() {
+// Default: K1x (variant 19) at k = 7, its k = 8 form (variant 24) at k = 8,
+// variant 1 (K1 / K2) elsewhere.
+int current_variant(int k) {
+    const int dflt = k == 8 ? kDefaultVariantK8 : kDefaultVariant;
     const char* e = getenv("KF_COUNT_VARIANT");
-    if (!e || !*e) return kDefaultVariant;
+    if (!e || !*e) return dflt;
     const int v = atoi(e);
-    return (v >= 0 && v < kNumVariants) ? v : kDefaultVariant;
+    return (v >= 0 && v < kNumVariants) ? v : dflt;
 }
 
 // Variant 22's claim tickets: one u32 per workgroup (kClaimStride apart), per
@@ -2455,7 +2571,7 @@ uint32_t wave_weights() {
 // kernel: P + S, nothing else
 int lds_bytes_for(int k, int v) {
     if (is_pair(k, v)) return (int)kPairLdsBytes;
-    if (is_static_pair(k, v)) return (int)kFwdSEnd;
+    if (is_static_pair(k, v) || is_k8x(k, v)) return (int)kFwdSEnd;
     if (is_dyn(k, v)) return (int)(sizeof(uint32_t) << (2 * k)) + 16;
     if (k <= kLdsMaxK) return (int)(sizeof(uint32_t) << (2 * k)) + 16 * 8;
     if (k <= kMultiMaxK) return (int)(sizeof(uint32_t) << kMultiBits) + 16 * 8;
@@ -2472,7 +2588,7 @@ int launch_info(int k, int* grid, int* block, int* lds, int* variant) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
     if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
-    const int v = current_variant();
+    const int v = current_variant(k);
     const int l = lds_bytes_for(k, v);
     std::lock_guard<std::mutex> lk(g_cache_mu);
     int& gr = g_cache.grid[k][v][dev];

@@ -532,3 +532,24 @@ def test_k7_stealing_repeated_launches(torch_dev, oracle, monkeypatch):
     for rep in range(3):
         counts, totals = run_batch(blobs, 7, torch_dev)
         check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"steal-{rep}")
+
+
+def test_k8_single_pass_kernel(torch_dev, oracle, monkeypatch):
+    """Variant 24: k = 8 on the K1x front end (every window an 8-mer in u16 LDS
+    counters, one pass): ragged FASTA with records, N runs, lowercase and CRLF;
+    low-complexity genomes whose u16 halves drain (poly-A, dinucleotide, an
+    8-mer palindrome repeat); many genome pieces per workgroup."""
+    monkeypatch.setenv("KF_COUNT_VARIANT", "24")
+    rng = np.random.default_rng(8088)
+    blobs = [gen.random_fasta(rng, int(rng.integers(0, 400_000)), max_records=5, n_rate=0.002, lower=0.05,
+                              crlf_rate=0.05, poly_rate=0.01) for _ in range(24)]
+    blobs += [b">polyA\n" + gen.wrap(np.frombuffer(b"A" * 12_000_000, np.uint8), 80),
+              b">ac\n" + gen.wrap(np.frombuffer(b"AC" * 3_000_000, np.uint8), 60),
+              b">pal\n" + gen.wrap(np.frombuffer(b"ACGTACGT" * 800_000, np.uint8), 80),
+              b">short\n" + gen.wrap(np.frombuffer(b"G" * 2_000_000, np.uint8), 7)]
+    counts, totals = run_batch(blobs, 8, torch_dev)
+    check_against_oracle(oracle, blobs, 8, counts, totals, tag="k8x")
+    blobs = [gen.random_fasta(rng, int(rng.integers(0, 40000)) if i % 37 else 0, max_records=40, n_rate=0.003,
+                              lower=0.05, crlf_rate=0.02, poly_rate=0.01) for i in range(600)]
+    counts, totals = run_batch(blobs, 8, torch_dev)
+    check_against_oracle(oracle, blobs, 8, counts, totals, tag="k8x-pieces")
