@@ -107,12 +107,19 @@ int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_gen
                    uint32_t* d_counts, uint64_t* d_totals, uint32_t flags, void* stream);
 
 /* Grid the count kernel will use on the current device for k (workgroups,
- * threads per workgroup, dynamic LDS bytes); for roofline accounting. */
+ * threads per workgroup, dynamic LDS bytes); for roofline accounting.
+ * Kernel choice: k = 7 K1x (KF_COUNT_VARIANT 19), k = 8 its single-pass form
+ * (24), k <= 6 K1 (1), k >= 9 the bucket kernels; KF_COUNT_VARIANT selects the
+ * measured alternatives (kf_count.hip lists them), for A/B runs only.  Variants
+ * 22 and 23 keep one small per-workgroup claim buffer per device and stream,
+ * allocated on first use. */
 int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
 
-/* Measurement aid (bench.py): read d_bytes[0, n) with the count kernel's access
- * pattern and XOR-fold it into *d_out (device).  Time it to get the practical
- * HBM read ceiling of that pattern.  Needs n rounded up to 16 readable. */
+/* Measurement aid (bench.py): read d_bytes[0, n) with the fastest read pattern
+ * measured on gfx950 (3 KiB blocks dealt grid-stride over the waves, coalesced
+ * 16-byte lanes, four blocks in flight per wave) and XOR-fold it into *d_out
+ * (device).  Time it to get the practical HBM read ceiling.  Needs n rounded up
+ * to 16 readable. */
 int kf_stream_probe(const uint8_t* d_bytes, uint64_t n, uint32_t* d_out, void* stream);
 
 /* Free the large-k workspace and tables of the current device (synchronises the
