@@ -67,7 +67,23 @@ def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
     return out
 
 
+def build_sanitized_host(out: str | None = None) -> str:
+    """SURVEY section 5 (sanitizers, host code only): the host half of the library
+    (csrc/kf_host.cpp) linked with the driver tests/host_sanitize.cpp under
+    AddressSanitizer + UndefinedBehaviorSanitizer (g++; no HIP in this binary)."""
+    out = out or os.path.join(BUILD, "host_sanitize")
+    os.makedirs(BUILD, exist_ok=True)
+    drv = os.path.join(HERE, "..", "tests", "host_sanitize.cpp")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-fno-omit-frame-pointer", "-Wall", "-Wextra", "-pthread", drv, os.path.join(CSRC, "kf_host.cpp"),
+                    "-o", out], check=True)
+    return out
+
+
 if __name__ == "__main__":
+    if "--sanitize" in sys.argv:
+        exe = build_sanitized_host()
+        sys.exit(subprocess.run([exe]).returncode)
     abl = "--ablation" in sys.argv
     print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, ablation=abl,
                 out=os.path.join(HERE, "libkf2vec_gpu_ablation.so") if abl else None))

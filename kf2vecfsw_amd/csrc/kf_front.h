@@ -519,7 +519,7 @@ __device__ __forceinline__ uint32_t wave_frac(uint32_t w, uint32_t wts) {
     cum += (s > 1 ? 4u * b1 : (s == 1 ? r * b1 : 0u));
     cum += (s > 2 ? 4u * b2 : (s == 2 ? r * b2 : 0u));
     cum += (s == 3 ? r * b3 : 0u);
-    return (cum << 20) / tot;   // cum <= 1020: no overflow
+    return (cum << 20) / tot;   // cum <= 15 x 255 = 3825 < 2^12: cum << 20 fits in u32
 }
 
 // [plo, phi) at fraction fr / 2^20 (phi - plo < 2^44), 16-byte aligned; the

@@ -134,16 +134,49 @@ def _spawn_shards(argv: list[str], world: int) -> int:
     return max(abs(p.wait()) for p in procs)
 
 
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without initialising HIP (the -gpus
+    parent forks children and must never touch the GPU itself): the first of
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES that is set,
+    capped by the GPU nodes of the KFD topology (nodes with SIMDs)."""
+    topo = "/sys/class/kfd/kfd/topology/nodes"
+    n_kfd = 0
+    try:
+        for d in os.listdir(topo):
+            try:
+                props = open(os.path.join(topo, d, "properties")).read().split("\n")
+            except OSError:
+                continue
+            if any(ln.startswith("simd_count") and ln.split()[-1] != "0" for ln in props):
+                n_kfd += 1
+    except OSError:
+        pass
+    n = n_kfd
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids)) if n_kfd else len(ids)
+            break
+    return n
+
+
 def get_frequencies(args) -> None:
     """kf2vec/main.py:250-373 on the GPU (-gpus N: byte-balanced file shards, one
     process per GPU)."""
     shard = _shard_spec(args)
     lead = shard is None or shard[0] == 0
+    if getattr(args, "gpus", 1) != 1 and int(os.environ.get("WORLD_SIZE", "1")) > 1 and not os.environ.get("KF_SHARD"):
+        # under torchrun every rank is already one shard: a -gpus spawn per rank
+        # would count the whole input on every rank and race on the same .kf files
+        raise ValueError("-gpus N cannot be combined with torchrun (WORLD_SIZE > 1): each rank counts its own shard")
     if shard is None and getattr(args, "gpus", 1) != 1:
         world = args.gpus
+        avail = visible_gpus()
         if world <= 0:
-            import torch
-            world = max(1, torch.cuda.device_count())   # (counting devices does not initialise them)
+            world = max(1, avail)
+        elif not os.environ.get("KF_SHARD_DEVICE") and world > avail:
+            raise ValueError("-gpus {}: only {} GPU(s) visible".format(world, avail))
         if world > 1:
             print("\n==> Starting k-mer counting for {}\n".format(args.input_dir))
             for d in (args.input_dir, args.output_dir):
@@ -179,6 +212,11 @@ def get_frequencies(args) -> None:
     import torch
     from .counter import KmerCounter, pack_files, to_device
 
+    if shard is not None and not os.environ.get("KF_SHARD"):
+        # torchrun: join the host-only gloo group now, before counting, so that a
+        # rank that fails later drops its connections and the others' final
+        # barrier errors out at once instead of waiting for a rendezvous timeout
+        _join_group()
     dflt = f"cuda:{os.environ.get('LOCAL_RANK', '0')}" if shard is not None else "cuda"
     device = torch.device(getattr(args, "device", None) or dflt)
     if not files_names:   # an empty shard
@@ -312,14 +350,23 @@ def get_frequencies(args) -> None:
     _finish(args, shard, lead)
 
 
+def _join_group() -> None:
+    """Host-only gloo group of the torchrun ranks (nothing on the data path)."""
+    import datetime
+
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # a rank may wait here for the slowest shard's counting: a long timeout
+        dist.init_process_group("gloo", timeout=datetime.timedelta(hours=6))
+
+
 def _finish(args, shard, lead: bool) -> None:
     """torchrun ranks meet in a gloo barrier (host only, nothing crosses) so rank 0
     prints the reference's last line after every shard is written."""
     if shard is not None and not os.environ.get("KF_SHARD"):
         import torch.distributed as dist
-        if not dist.is_initialized():
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo")
+        _join_group()
         dist.barrier()
     if lead and not os.environ.get("KF_SHARD"):
         print("\n==> Done processing {}".format(args.input_dir))

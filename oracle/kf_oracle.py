@@ -50,6 +50,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_vocab.argtypes = [i32, vp]
         L.oracle_count.argtypes = [vp, u64, i32, i32, vp, vp, vp]
         L.oracle_count_many.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, i32]
+        L.oracle_count_many_parts.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, i32, u64]
         L.oracle_max_threads.restype = i32
         L.oracle_synth_header_len.restype = u64
         L.oracle_synth_header_len.argtypes = [ctypes.c_int64]
@@ -101,6 +102,20 @@ def count_many(buf: np.ndarray, off: np.ndarray, k: int, fmt: int = 0, threads: 
     t = np.zeros(n, dtype=np.uint64)
     assert lib().oracle_count_many(_ptr(buf), _ptr(off), n, k, fmt, _ptr(rank_std(k)),
                                    _ptr(c), _ptr(t), threads) == 0
+    return c, t
+
+
+def count_many_parts(buf: np.ndarray, off: np.ndarray, k: int, fmt: int = 0, threads: int = 0,
+                     part_bytes: int = 1 << 20):
+    """As count_many, OpenMP over (genome, part) pairs of about part_bytes each
+    (bench.py's CPU baseline: every host thread busy whatever the genome count)."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    n = off.size - 1
+    c = np.zeros((n, nbins(k)), dtype=np.uint32)
+    t = np.zeros(n, dtype=np.uint64)
+    assert lib().oracle_count_many_parts(_ptr(buf), _ptr(off), n, k, fmt, _ptr(rank_std(k)),
+                                         _ptr(c), _ptr(t), threads, part_bytes) == 0
     return c, t
 
 

@@ -193,6 +193,119 @@ int oracle_count_many(const uint8_t* bytes, const uint64_t* off, int n_genomes, 
     return 0;
 }
 
+/* FASTA scan of bytes [from, n) that counts only the k-mers ending at bytes in
+ * [a, e).  `from` must be a line start (or 0); the bytes [from, a) only rebuild
+ * the k-mer context and the header state, exactly as scan_fasta would have them
+ * at a (a record boundary or non-ACGT byte in between resets it the same way). */
+static void scan_fasta_part(kstate* s, const uint8_t* b, uint64_t from, uint64_t a, uint64_t e) {
+    int at_line_start = 1, in_header = 0;
+    for (uint64_t i = from; i < e; ++i) {
+        uint8_t c = b[i];
+        if (at_line_start && c == '>') { in_header = 1; ks_reset(s); }
+        at_line_start = (c == '\n');
+        if (c == '\n') { in_header = 0; continue; }
+        if (in_header) continue;
+        if (i < a) {   /* context only: push without counting */
+            int code = std_code(c);
+            if (code < 0) { s->len = 0; continue; }
+            s->fw = ((s->fw << 2) | (uint64_t)code) & s->mask;
+            s->rc = (s->rc >> 2) | ((uint64_t)(3 - code) << (2 * s->k - 2));
+            ++s->len;
+            continue;
+        }
+        ks_push(s, c);
+    }
+}
+
+/* As oracle_count_many, with every FASTA genome cut into parts of about
+ * `part_bytes` bytes and OpenMP over all (genome, part) pairs, so that the
+ * threads are not capped by the number of genomes (bench.py's CPU baseline on
+ * the GPU box's nproc threads).  Part j of a genome counts the k-mers whose
+ * last base lies in its byte range; it rebuilds its context by scanning from
+ * the start of the line holding the k-th non-newline byte before the range (a
+ * FASTA line start is a state-free restart point).  FASTQ genomes are one part each.
+ * Each part counts into a thread-private row, added to the genome's row under
+ * an atomic per non-zero bin. */
+int oracle_count_many_parts(const uint8_t* bytes, const uint64_t* off, int n_genomes, int k, int fmt,
+                            const uint32_t* rank_std, uint32_t* counts, uint64_t* totals, int n_threads,
+                            uint64_t part_bytes) {
+    uint64_t nb = oracle_nbins(k);
+    if (!nb || part_bytes == 0) return -1;
+    uint64_t* first = (uint64_t*)malloc(((size_t)n_genomes + 1) * sizeof(uint64_t));
+    if (!first) return -1;
+    first[0] = 0;
+    for (int g = 0; g < n_genomes; ++g) {
+        const uint64_t len = off[g + 1] - off[g];
+        const int fq = sniff(bytes + off[g], len, fmt) == 2;
+        const uint64_t np = (fq || len == 0) ? 1 : (len + part_bytes - 1) / part_bytes;
+        first[g + 1] = first[g] + np;
+        memset(counts + (uint64_t)g * nb, 0, nb * sizeof(uint32_t));
+        totals[g] = 0;
+    }
+    const int64_t ntask = (int64_t)first[n_genomes];
+    int rc = 0;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel
+#endif
+    {
+        uint32_t* loc = (uint32_t*)calloc(nb, sizeof(uint32_t));
+        if (!loc) {
+#ifdef _OPENMP
+#pragma omp atomic write
+#endif
+            rc = -1;
+        }
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t t = 0; t < ntask; ++t) {
+            if (!loc) continue;
+            int g = 0, lo = 0, hi = n_genomes;   /* genome of task t: last g with first[g] <= t */
+            while (hi - lo > 1) { int m = (lo + hi) / 2; if (first[m] <= (uint64_t)t) lo = m; else hi = m; }
+            g = lo;
+            const uint8_t* b = bytes + off[g];
+            const uint64_t len = off[g + 1] - off[g], np = first[g + 1] - first[g], j = (uint64_t)t - first[g];
+            kstate s;
+            memset(&s, 0, sizeof s);
+            s.k = k;
+            s.mask = (1ull << (2 * k)) - 1;
+            s.rank = rank_std;
+            s.counts = loc;
+            if (np == 1) {
+                if (sniff(b, len, fmt) == 2) scan_fastq(&s, b, len);
+                else scan_fasta(&s, b, len);
+            } else {
+                const uint64_t a = len / np * j + (len % np) * j / np;
+                const uint64_t e = j + 1 == np ? len : len / np * (j + 1) + (len % np) * (j + 1) / np;
+                /* back over k non-newline bytes (k bases of context, or a reset
+                 * among them), then to the start of that line */
+                uint64_t from = a;
+                for (int seen = 0; from > 0 && seen < k;)
+                    if (b[--from] != '\n') ++seen;
+                while (from > 0 && b[from - 1] != '\n') --from;
+                scan_fasta_part(&s, b, from, a, e);
+            }
+            uint32_t* row = counts + (uint64_t)g * nb;
+            for (uint64_t i = 0; i < nb; ++i) {
+                if (!loc[i]) continue;
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+                row[i] += loc[i];
+                loc[i] = 0;
+            }
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+            totals[g] += s.total;
+        }
+        free(loc);
+    }
+    free(first);
+    return rc;
+}
+
 int oracle_max_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

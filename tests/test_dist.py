@@ -34,6 +34,55 @@ def _worker(rank, world, port, n, q):
     dist.destroy_process_group()
 
 
+def _plan_worker(rank, world, port, total, per, q):
+    """One rank of bench.py's configs[3] run: its sub-batch plan, the ids it would
+    generate, and the all-gathered plans of every rank."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    plan = bench.shard_plan(total, rank, world, per)
+    mine = sorted(a + i * st for a, st, c in plan for i in range(c))
+    n_sb = torch.tensor([float(len(plan))])
+    dist.all_reduce(n_sb, op=dist.ReduceOp.MAX)
+    counts = [None] * world
+    dist.all_gather_object(counts, [c for _, _, c in plan])
+    q.put((rank, mine, len(plan), float(n_sb), counts))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_configs3_50k_shards_disjoint_and_complete(world):
+    """bench.py's N>1 workload (BASELINE configs[3]): the 50,000 genome ids are
+    split round-robin (genome g on rank g mod N) into per-rank sub-batches of at
+    most 6,250; over the ranks of a gloo group the ids are disjoint and complete,
+    each rank's are exactly g % N == r, and every rank has the same number of
+    sub-batches (the streamed mode's barriers line up)."""
+    import bench
+    total, per = bench.CONFIG3_GENOMES, bench.SUB_BATCH
+    if world == 1:
+        plan = bench.shard_plan(total, 0, 1, per)
+        ids = [a + i * st for a, st, c in plan for i in range(c)]
+        assert ids == list(range(total)) and len(plan) == 8 and all(c <= per for _, _, c in plan)
+        return
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, world, port, total, per, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    all_ids = [i for _, mine, _, _, _ in res for i in mine]
+    assert len(all_ids) == total and sorted(all_ids) == list(range(total))
+    for rank, mine, nsb, nsb_max, counts in res:
+        assert mine == list(range(rank, total, world))
+        assert nsb == nsb_max == -(-(total // world) // per)
+        assert all(c <= per for row in counts for c in row)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_round_robin_shards_cover_all_genomes(world):
     n = 7
@@ -93,3 +142,24 @@ def test_cli_shard_spec_from_env(monkeypatch):
     assert _shard_spec(SimpleNamespace(gpus=4)) is None         # -gpus spawns its own children
     monkeypatch.setenv("KF_SHARD", "3,8")
     assert _shard_spec(SimpleNamespace(gpus=1)) == (3, 8)       # a -gpus child
+
+
+def test_cli_gpus_validation(monkeypatch, tmp_path):
+    """-gpus N under torchrun is refused (every rank would count everything); -gpus
+    larger than the visible GPUs is refused; visible_gpus reads the env masks
+    without initialising HIP."""
+    from kf2vecfsw_amd import main as M
+    monkeypatch.delenv("KF_SHARD", raising=False)
+    monkeypatch.delenv("KF_SHARD_DEVICE", raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    n = M.visible_gpus()
+    assert n <= 2
+    a = M.build_parser().parse_args(["get_frequencies", "-input_dir", str(tmp_path), "-output_dir", str(tmp_path),
+                                     "-gpus", "4"])
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(ValueError, match="torchrun"):
+        M.get_frequencies(a)
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    with pytest.raises(ValueError, match="visible"):
+        M.get_frequencies(a)

@@ -83,3 +83,22 @@ def test_oracle_synth_spec(oracle):
     assert set(b"".join(lines[1:])) <= set(b"ACGT")
     gn = oracle.synth_genome(3, 7, 300000, 80, n_period=2)
     assert b"N" in gn
+
+
+@pytest.mark.parametrize("part", [3, 64, 1000, 1 << 20])
+def test_oracle_parts_equal_whole_genomes(oracle, part):
+    """bench.py's CPU baseline counts each genome in parts (OpenMP over genome x
+    part, context rebuilt from a line start): it must equal the per-genome scan on
+    ragged FASTA (headers, blank lines, 1-base lines, N, CRLF, lowercase) and FASTQ."""
+    import gen
+    rng = np.random.default_rng(31 + part)
+    blobs = [gen.random_fasta(rng, int(rng.integers(0, 12000)), max_records=6, n_rate=0.003, lower=0.05,
+                              crlf_rate=0.1, iupac_rate=0.001, poly_rate=0.01) for _ in range(12)]
+    blobs += [b"", b">h\n", b"\n\n\n\n", b">x\n" + b"\n" * 50 + b"ACGTACGTAC\n" * 3 + b"\n" * 40 + b"GGTTACA\n",
+              gen.random_fastq(rng, 50, n_rate=0.01)]
+    off = np.cumsum([0] + [len(b) for b in blobs]).astype(np.uint64)
+    buf = np.frombuffer(b"".join(blobs) + b"\0", np.uint8)
+    for k in ((3, 7) if part < 1000 else (3, 7, 11)):   # (each part merges a whole row)
+        c1, t1 = oracle.count_many(buf, off, k, 0, 4)
+        c2, t2 = oracle.count_many_parts(buf, off, k, 0, 4, part)
+        assert np.array_equal(c1, c2) and np.array_equal(t1, t2), (k, part)
