@@ -257,10 +257,16 @@ uint64_t format_line(const char* name, const uint32_t* c, uint64_t nb, int pseud
         sum += (double)c[i];        // exact: integers < 2^53
     }
     if (pseudo) sum += 0.5 * (double)nb;   // exact: multiples of 0.5 < 2^53
+    // Integer text ("54", not "54.0") in raw mode without pseudocount when the
+    // merged column is not float64: every vocab k-mer is in the dump (pd.merge
+    // keeps the dump's int64 column), or the dump is empty (an object column of
+    // NaN, which fillna(0) fills with the int 0).  Pinned by
+    // tests/golden/ref_postproc (dense_k3_raw, empty_k7_raw).
+    const bool int_text = raw && !pseudo && (all_present || sum == 0.0);
     for (uint64_t i = 0; i < nb; ++i) {
         if (i) *p++ = ',';
-        if (raw && !pseudo && all_present) {
-            p = fmt_u64(c[i], p);   // int64 column (no NaN from the merge)
+        if (int_text) {
+            p = fmt_u64(c[i], p);
         } else {
             double v = (double)c[i] + (pseudo ? 0.5 : 0.0);
             if (!raw) v = v / sum;

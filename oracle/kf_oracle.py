@@ -135,13 +135,16 @@ def synth_genome(g: int, seed: int, seq_len: int, width: int = 80, n_period: int
 def kf_values(counts: np.ndarray, pseudocount: bool = False, raw_cnt: bool = False) -> list[str]:
     """``my_merged_counts["counts"].astype(str).to_list()`` (main.py:327-345).
 
-    dtype quirk of the reference: ``pd.merge(vocab, dump, how='left')`` keeps the
+    dtype quirks of the reference: ``pd.merge(vocab, dump, how='left')`` keeps the
     int64 dtype of the dump's count column when every vocab k-mer is present in
     the dump (no NaN introduced), otherwise it becomes float64 (NaN -> fillna(0)).
     So raw counts print as "54" when no bin is empty and "54.0" otherwise.
     """
     c = np.asarray(counts, dtype=np.int64)
-    is_int = bool(c.size) and bool((c > 0).all())
+    # ... and an empty dump (no k-mer at all): pandas reads an object column, the
+    # merge leaves NaN everywhere and fillna(0) fills in the int 0, so raw counts
+    # print "0" (pinned by tests/golden/ref_postproc/kf/empty_k7_raw.kf.gz)
+    is_int = bool(c.size) and (bool((c > 0).all()) or not c.any())
     if pseudocount:                                   # main.py:332-334
         v = c.astype(np.float64) + 0.5
         is_int = False

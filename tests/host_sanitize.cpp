@@ -139,7 +139,7 @@ static void format(std::mt19937_64& rng) {
                 for (uint64_t i = 0; i < f.size() && i < nb; ++i) {
                     double v = c[i] + (pseudo ? 0.5 : 0.0);
                     if (!raw) v = v / sum;
-                    if (raw && !pseudo && all) {
+                    if (raw && !pseudo && (all || sum == 0.0)) {
                         CHECK(f[i] == std::to_string(c[i]));
                     } else if (v != v) {
                         CHECK(f[i] == "nan");

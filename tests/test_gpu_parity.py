@@ -553,3 +553,101 @@ def test_k8_single_pass_kernel(torch_dev, oracle, monkeypatch):
                               lower=0.05, crlf_rate=0.02, poly_rate=0.01) for i in range(600)]
     counts, totals = run_batch(blobs, 8, torch_dev)
     check_against_oracle(oracle, blobs, 8, counts, totals, tag="k8x-pieces")
+
+
+def test_cli_modes_match_reference_postproc(torch_dev, tmp_path):
+    """`get_frequencies` with -pseudocount, -raw_cnt and both (and neither) on the
+    inputs of tests/golden/ref_postproc -- ragged multi-record, every-bin-present,
+    tiny, low-complexity and EMPTY genomes at k = 3..9 -- writes the bytes the
+    reference's own post-processing wrote (kf2vec/main.py:323-357, run in the
+    build container by tests/golden/ref_postproc/make_fixtures.py)."""
+    import json
+    from conftest import GOLDEN
+    from kf2vecfsw_amd import main as M
+    d = os.path.join(GOLDEN, "ref_postproc")
+    man = json.load(open(os.path.join(d, "manifest.json")))
+    cases = man["kf"] + [e for e in man["errors"] if "file" in e]
+    groups = {}
+    for e in cases:
+        groups.setdefault((e["k"], e["pseudocount"], e["raw_cnt"]), []).append(e)
+    n = 0
+    for (k, pseudo, raw), es in sorted(groups.items()):
+        inp, out = tmp_path / f"in{k}{pseudo:d}{raw:d}", tmp_path / f"out{k}{pseudo:d}{raw:d}"
+        inp.mkdir()
+        out.mkdir()
+        for e in es:
+            data = gzip.open(os.path.join(d, e["input"])).read() if "input" in e else b""
+            (inp / (e.get("sample", "empty") + ".fna")).write_bytes(data)
+        argv = ["get_frequencies", "-input_dir", str(inp), "-output_dir", str(out), "-k", str(k), "-p", "2"]
+        M.main(argv + (["-pseudocount"] if pseudo else []) + (["-raw_cnt"] if raw else []))
+        for e in es:
+            exp = gzip.open(os.path.join(d, e["file"])).read()
+            assert (out / (e.get("sample", "empty") + ".kf")).read_bytes() == exp, e["file"]
+            n += 1
+    assert n == 44
+
+
+def test_cli_get_kmers_matches_reference_npy(torch_dev, tmp_path):
+    """`get_kmers` .npy of tests/golden/ref_postproc (the reference's main.py:147-176
+    on its dump) equal bit for bit (rows in the sorted order the fixture's dump used)."""
+    import json
+    from conftest import GOLDEN
+    from kf2vecfsw_amd import main as M
+    d = os.path.join(GOLDEN, "ref_postproc")
+    man = json.load(open(os.path.join(d, "manifest.json")))
+    for k in sorted({e["k"] for e in man["npy"]}):
+        inp, out = tmp_path / f"in{k}", tmp_path / f"out{k}"
+        inp.mkdir()
+        es = [e for e in man["npy"] if e["k"] == k]
+        for e in es:
+            name = os.path.basename(e["input"])[: -len(".fna.gz")]
+            (inp / (name + ".fna")).write_bytes(gzip.open(os.path.join(d, e["input"])).read())
+        M.main(["get_kmers", "-input_dir", str(inp), "-output_dir", str(out), "-k", str(k)])
+        for e in es:
+            exp = np.load(os.path.join(d, e["file"]), allow_pickle=False)
+            got = np.load(out / os.path.basename(e["file"]), allow_pickle=False)
+            assert got.dtype == exp.dtype and np.array_equal(got, exp), e["file"]
+
+
+def _bacterial_like(rng, total):
+    """BASELINE configs[2] stand-in (no bacterial assemblies offline): 1-80 contigs,
+    GC 30-70 %, N runs, 60/80-column lines, soft-masked stretches."""
+    ncontig = int(rng.integers(1, 81))
+    cuts = np.sort(rng.choice(np.arange(1, total), size=ncontig - 1, replace=False)) if ncontig > 1 else []
+    lens = np.diff(np.concatenate([[0], cuts, [total]]))
+    gc = float(rng.uniform(0.3, 0.7))
+    width = int(rng.choice([60, 80]))
+    out = []
+    for i, L in enumerate(lens):
+        seq = gen.random_seq(rng, int(L), gc=gc, n_rate=2e-5)
+        if rng.random() < 0.3 and L > 2000:
+            a = int(rng.integers(0, L - 1000))
+            seq[a: a + 1000] |= 0x20
+        out.append(b">contig_%d len=%d\n" % (i, L) + gen.wrap(seq, width))
+    return b"".join(out)
+
+
+def test_cli_64_bacterial_like_genomes(torch_dev, oracle, tmp_path):
+    """BASELINE configs[2]: 64 bacterial-like ~5 Mbp genomes through the CLI
+    (pipelined batches, threaded writer); every `.kf` byte-exact vs the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    from kf2vecfsw_amd import main as M
+    rng = np.random.default_rng(2026)
+    inp, out = tmp_path / "in", tmp_path / "out"
+    inp.mkdir()
+    out.mkdir()
+    blobs = {}
+    for g in range(64):
+        b = _bacterial_like(rng, 5_000_000)
+        blobs[f"B{g:04d}"] = b
+        (inp / f"B{g:04d}.fna").write_bytes(b)
+    M.main(["get_frequencies", "-input_dir", str(inp), "-output_dir", str(out), "-k", "7", "-p", "16"])
+
+    def check(item):
+        name, b = item
+        c, _ = oracle.count(b, 7)
+        return name, (out / f"{name}.kf").read_bytes() == oracle.kf_line(name, c).encode()
+
+    with ThreadPoolExecutor(8) as ex:
+        bad = [nm for nm, ok in ex.map(check, blobs.items()) if not ok]
+    assert not bad, bad

@@ -102,3 +102,65 @@ def test_oracle_parts_equal_whole_genomes(oracle, part):
         c1, t1 = oracle.count_many(buf, off, k, 0, 4)
         c2, t2 = oracle.count_many_parts(buf, off, k, 0, 4, part)
         assert np.array_equal(c1, c2) and np.array_equal(t1, t2), (k, part)
+
+
+# ---------------------------------------------------------------------------
+# tests/golden/ref_postproc: the reference's own get_frequencies / get_kmers
+# post-processing (kf2vec/main.py:250-373, 112-184), run in the build container
+# by tests/golden/ref_postproc/make_fixtures.py on inputs the toy set lacks
+# ---------------------------------------------------------------------------
+REFPP = os.path.join(GOLDEN, "ref_postproc")
+
+
+def _refpp():
+    return json.load(open(os.path.join(REFPP, "manifest.json")))
+
+
+def _refpp_input(rel):
+    return gzip.open(os.path.join(REFPP, rel)).read()
+
+
+def test_refpp_kf_modes_oracle_and_product_formatter(oracle):
+    """-pseudocount, -raw_cnt, both, on ragged / all-bins-present / tiny /
+    low-complexity genomes at k = 3..9, plus the empty genome: the oracle's
+    restatement AND the product's C++ formatter (kf_format_kf, host code) give the
+    reference's bytes."""
+    from kf2vecfsw_amd.main import format_kf
+    m = _refpp()
+    cases = m["kf"] + [e for e in m["errors"] if "file" in e]
+    assert len(cases) == 44
+    for e in cases:
+        exp = gzip.open(os.path.join(REFPP, e["file"])).read()
+        data = _refpp_input(e["input"]) if "input" in e else b""
+        name = e.get("sample", "empty")
+        c, _ = oracle.count(data, e["k"])
+        assert oracle.kf_line(name, c, e["pseudocount"], e["raw_cnt"]).encode() == exp, e["file"]
+        assert format_kf(name, c, e["pseudocount"], e["raw_cnt"]) == exp, e["file"]
+
+
+def test_refpp_int_text_quirks_are_covered():
+    """The fixtures hold both integer-text cases of raw mode (every bin present;
+    empty dump) and their float counterparts."""
+    m = _refpp()
+    firsts = {e["file"]: gzip.open(os.path.join(REFPP, e["file"])).read().split(b",")[1]
+              for e in m["kf"] + [e for e in m["errors"] if "file" in e]}
+    assert firsts["kf/dense_k3_raw.kf.gz"].isdigit()
+    assert firsts["kf/empty_k7_raw.kf.gz"] == b"0"
+    assert firsts["kf/empty_k7.kf.gz"] == b"nan"
+    assert b"." in firsts["kf/ragged_k7_raw.kf.gz"] and b"." in firsts["kf/dense_k3_pseudo_raw.kf.gz"]
+
+
+def test_refpp_npy_oracle_and_product(oracle):
+    """get_kmers .npy: digits A0 T1 C2 G3 + float32 count / float32 sum, rows in
+    the dump's order (sorted canonical here): the oracle's restatement and the
+    product's kmers_matrix equal the reference's arrays bit for bit."""
+    from kf2vecfsw_amd.main import kmers_matrix
+    m = _refpp()
+    assert len(m["npy"]) == 6
+    for e in m["npy"]:
+        exp = np.load(os.path.join(REFPP, e["file"]), allow_pickle=False)
+        c, _ = oracle.count(_refpp_input(e["input"]), e["k"])
+        ref = oracle.kmers_matrix_from_dump(oracle.dump_lines(c, e["k"]), e["k"])
+        assert exp.dtype == np.float32 and np.array_equal(ref, exp), e["file"]
+        got = kmers_matrix(c, e["k"])
+        assert got.dtype == np.float32 and np.array_equal(got, exp), e["file"]
