@@ -143,7 +143,8 @@ uint64_t kf_synth_header_len(int64_t g);
  *   "<name>," + ",".join(str(v)) + "\n"
  * with v = counts (+0.5 if pseudocount) (/ sum unless raw_cnt), float64,
  * printed like Python repr(float); raw counts with no empty bin print as
- * integers (pandas keeps int64 when the left-merge introduces no NaN).
+ * integers (pandas keeps int64 when the left-merge introduces no NaN), and so
+ * do the zeros of a genome with no k-mer at all (an empty dump).
  * On KF_ERANGE *written is the size needed. */
 int kf_format_kf(const char* name, const uint32_t* counts, uint64_t nbins,
                  int pseudocount, int raw_cnt, char* out, uint64_t cap, uint64_t* written);
@@ -153,6 +154,31 @@ int kf_format_kf(const char* name, const uint32_t* counts, uint64_t nbins,
 int kf_write_kf_files(const char* dir, const char* const* names, int32_t n,
                       const uint32_t* counts, uint64_t nbins, int pseudocount,
                       int raw_cnt, int n_threads);
+
+/* get_chunks (main.py:869-915): the rows of many windows in ONE file, in order:
+ * path = the file, row i = names[i] + counts row i, formatted by n_threads host
+ * threads (as kf_format_kf) and written in row order. */
+int kf_write_kf_rows(const char* path, const char* const* names, int32_t n,
+                     const uint32_t* counts, uint64_t nbins, int pseudocount,
+                     int raw_cnt, int n_threads);
+
+/* ---- get_chunks device pre-pass (replaces seqtk seq -l 0 | awk N-collapse |
+ * seqkit seq -g -m, main.py:726-760).  d_seq holds n_rec sorted, disjoint
+ * [start, end) byte ranges of record sequences (the bytes between a header's
+ * '\n' and the next header).  Writes each record's processed sequence --
+ * newlines and line-end '\r' dropped, the gap letters "- \t." dropped, runs of
+ * N / n / '|' (awk runs before seqkit: gap letters split a run) collapsed to
+ * one 'N' -- back to back into d_out (>= len bytes) and its [start, end) into
+ * d_out_se[2r], d_out_se[2r+1].  d_scratch: >= ceil(len / 4096) + 1 words.
+ * Asynchronous on `stream`. */
+int kf_chunk_compact(const uint8_t* d_bytes, uint64_t len, const uint64_t* d_seq, int32_t n_rec,
+                     uint8_t* d_out, uint64_t* d_out_se, uint32_t* d_scratch, uint64_t scratch_words,
+                     void* stream);
+
+/* Window w = d_src[d_win_src[w], + win_len) to d_dst[w * win_len, + win_len)
+ * (the seqkit sliding windows of main.py:813-824, laid out for kf_count_batch). */
+int kf_chunk_gather(const uint8_t* d_src, const uint64_t* d_win_src, int32_t n_win, uint32_t win_len,
+                    uint8_t* d_dst, void* stream);
 
 #ifdef __cplusplus
 }

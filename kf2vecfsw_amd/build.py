@@ -17,7 +17,7 @@ BUILD = os.path.join(HERE, "_build")
 ARCH = os.environ.get("KF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES_HIP = ["kf_count.hip", "kf_bucket.hip"]
+SOURCES_HIP = ["kf_count.hip", "kf_bucket.hip", "kf_chunks.hip"]
 SOURCES_CPP = ["kf_host.cpp"]
 DEPS = SOURCES_HIP + SOURCES_CPP + ["kf_internal.h", "kf_front.h", "../../include/kf2vec_gpu.h"]
 
@@ -30,7 +30,8 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, ablation: bool = False, out: str | None = None) -> str:
-    """ablation=True adds profiling-only kernel variants (KF_COUNT_VARIANT 3, 4).
+    """ablation=True: a profiling build of the product (KF_PROFILE_BUILD: the
+    bucket kernels' KF_BUCKET_PROFILE / KF_BK_WEIGHTS knobs).
     Serialised by a file lock: every rank of a multi-process run may call it."""
     import fcntl
     out = out or OUT
@@ -49,7 +50,7 @@ def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
     for s in SOURCES_HIP:
         o = os.path.join(BUILD, s + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-c", os.path.join(CSRC, s), "-o", o] + (["-DKF_ABLATION"] if ablation else [])
+               "-c", os.path.join(CSRC, s), "-o", o] + (["-DKF_PROFILE_BUILD"] if ablation else [])
         cmd += os.environ.get("KF_HIPCC_FLAGS", "").split()   # tools/ only (profiling ablations)
         if verbose:
             cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
@@ -80,7 +81,33 @@ def build_sanitized_host(out: str | None = None) -> str:
     return out
 
 
+def build_zoo() -> str:
+    """tools/zoo/libkf2vec_zoo.so: the round-2 library with every rejected k <= 8
+    kernel variant (KF_COUNT_VARIANT, KF_COUNT_PROFILE, KF_BUCKET_MIN_K knobs),
+    for tools/ measurements only -- never loaded by the product (KF2VEC_GPU_LIB)."""
+    zoo = os.path.join(HERE, "..", "tools", "zoo")
+    out = os.path.join(zoo, "libkf2vec_zoo.so")
+    bld = os.path.join(BUILD, "zoo")
+    os.makedirs(bld, exist_ok=True)
+    objs = []
+    for s in ["kf_count_zoo.hip", "kf_bucket_zoo.hip"]:
+        o = os.path.join(bld, s + ".o")
+        subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-DKF_ABLATION",
+                        "-DKF_PROFILE_BUILD", "-I", CSRC, "-c", os.path.join(zoo, s), "-o", o]
+                       + os.environ.get("KF_HIPCC_FLAGS", "").split(), check=True)
+        objs.append(o)
+    o = os.path.join(bld, "kf_host.cpp.o")
+    subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", "-c", os.path.join(CSRC, "kf_host.cpp"), "-o", o],
+                   check=True)
+    objs.append(o)
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs, "-o", out], check=True)
+    return out
+
+
 if __name__ == "__main__":
+    if "--zoo" in sys.argv:
+        print(build_zoo())
+        sys.exit(0)
     if "--sanitize" in sys.argv:
         exe = build_sanitized_host()
         sys.exit(subprocess.run([exe]).returncode)

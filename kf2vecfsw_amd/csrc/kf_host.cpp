@@ -330,6 +330,34 @@ extern "C" int kf_write_kf_files(const char* dir, const char* const* names, int3
     return KF_OK;
 }
 
+extern "C" int kf_write_kf_rows(const char* path, const char* const* names, int32_t n, const uint32_t* counts,
+                                uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
+    if (!path || (!names && n) || (!counts && n) || n < 0) return kf_fail(KF_EINVAL, "null argument");
+    if (n_threads < 1) n_threads = 1;
+    n_threads = std::min<int>(n_threads, std::max<int32_t>(n, 1));
+    std::vector<std::vector<char>> rows((size_t)n);
+    std::vector<uint64_t> len((size_t)n, 0);
+    std::atomic<int32_t> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const int32_t i = next.fetch_add(1);
+            if (i >= n) break;
+            rows[i].resize(kf_line_cap(strlen(names[i]), nbins));
+            len[i] = format_line(names[i], counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt, rows[i].data());
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < n_threads; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    FILE* f = fopen(path, "wb");
+    bool ok = f != nullptr;
+    for (int32_t i = 0; ok && i < n; ++i) ok = fwrite(rows[i].data(), 1, len[i], f) == len[i];
+    if (f) ok = (fclose(f) == 0) && ok;
+    if (!ok) return kf_fail(KF_EINVAL, "cannot write %s", path);
+    return KF_OK;
+}
+
 // ------------------------------------------------------------------ synthetic layout
 extern "C" uint64_t kf_synth_header_len(int64_t g) {
     char tmp[32];

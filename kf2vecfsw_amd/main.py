@@ -465,14 +465,17 @@ def _hms(seconds: float) -> tuple[int, int, int]:
 
 
 def get_chunks(args) -> None:
-    """kf2vec/main.py:654-929: one device batch of all windows of a group of
-    genomes instead of one Jellyfish pair per 10 kbp window."""
+    """kf2vec/main.py:654-929: each genome's records are linearised, N-collapsed
+    and gap-filtered on the device (kf_chunk_compact), its 10 kbp windows are
+    gathered into a device batch with other genomes' windows, and one
+    kf_count_batch counts the batch -- instead of seqtk + awk + seqkit per genome
+    and one Jellyfish pair per window."""
     import logging
     import time
 
     import torch
     from . import chunks as CH
-    from .counter import KmerCounter, counts_to_numpy, pack_genomes, to_device
+    from .counter import KmerCounter
 
     since = time.time()
     if not os.path.exists(args.input_dir):
@@ -500,50 +503,31 @@ def get_chunks(args) -> None:
             args.k, supported_k.start, supported_k.stop - 1))
     device = torch.device(getattr(args, "device", None) or "cuda")
     counter = KmerCounter(args.k, device)
-    budget = int(float(getattr(args, "batch_gb", 4.0) or 4.0) * (1 << 30))
+    budget = int(float(getattr(args, "batch_gb", 1.0) or 1.0) * (1 << 30))
+    pipe = CH.ChunkPipeline(counter, device, max(1, budget // CH.CHUNK_SZ), args.p)
+    fname_of = dict(zip(samples_names, files_names))
 
-    pending: list[tuple[str, list[tuple[str, bytes]]]] = []
-    pending_bytes = 0
+    def written(sample):
+        stamp("\n==> Done computing k-mer frequences for {}.".format(fname_of.get(sample, sample)))
 
-    def flush_pending():
-        nonlocal pending, pending_bytes
-        if not pending:
-            return
-        blobs, names = [], []
-        for _, wins in pending:
-            for nm, seq in wins:
-                names.append(nm)
-                blobs.append(seq)
-        counts, _ = counter.count(to_device(pack_genomes(blobs, names), device))
-        c = counts_to_numpy(counts)
-        row = 0
-        for sample, wins in pending:
-            lines = [format_kf(nm, c[row + j], args.pseudocount, True) for j, (nm, _) in enumerate(wins)]
-            row += len(wins)
-            with open(os.path.join(args.output_dir, "{}.kf".format(sample)), "wb") as f:
-                f.write(b"".join(lines))
-            stamp("\n==> Done computing k-mer frequences for {}.".format(
-                dict((s, fn) for fn, s in zip(files_names, samples_names)).get(sample, sample)))
-        pending, pending_bytes = [], 0
+    def flush():
+        pipe.count_and_write(args.output_dir, args.pseudocount, written)
 
     for fname, sample in zip(files_names, samples_names):
         log.info("\n==> Start processing. Sample: {}".format(fname))
         with open(os.path.join(args.input_dir, fname), "rb") as f:
             data = f.read()
-        wins = CH.genome_windows(data, sample)
-        if not wins:   # no contig of >= 10 kbp after N-collapse / gap removal (main.py:761-778)
+        names, starts, d_seq = pipe.windows_of(data, sample)
+        if not names:   # no contig of >= 10 kbp after N-collapse / gap removal (main.py:761-778)
             stamp("\n==> Excluded {}. No contigs above threshold length.".format(fname))
             continue
-        if len(wins) < CH.CHUNK_CNT_THR:                                   # main.py:845-860
+        if len(names) < CH.CHUNK_CNT_THR:                                  # main.py:845-860
             stamp("\n==> Excluded {}. {} chunks is too low. {} is required.".format(
-                fname, len(wins), CH.CHUNK_CNT_THR))
+                fname, len(names), CH.CHUNK_CNT_THR))
             continue
         stamp("\n==> Done chunk processing for {}.".format(fname))
-        pending.append((sample, wins))
-        pending_bytes += len(wins) * CH.CHUNK_SZ
-        if pending_bytes >= budget:
-            flush_pending()
-    flush_pending()
+        pipe.add(sample, names, starts, d_seq, flush)
+    flush()
     stamp("\n==> Done getting chunks.")
 
 

@@ -329,33 +329,32 @@ def test_bucket_mixed_batch_and_accumulate(torch_dev, oracle, k):
 
 
 @pytest.mark.parametrize("k", [9, 10])
-def test_bucket_kernel_agrees_with_other_large_k_paths(torch_dev, monkeypatch, k):
-    """k=9: bucket vs multi-pass LDS; k=10: bucket vs global atomics (KF_BUCKET_MIN_K)."""
+def test_bucket_kernel_synth_batch_vs_oracle(torch_dev, oracle, k):
+    """k = 9, 10 bucket kernels on a device-generated batch with N runs: every
+    total analytic-consistent and sampled genomes bit-exact vs the oracle."""
     import torch
     from kf2vecfsw_amd import counter as C
     db = C.synth_device_batch(40, 700_000, seed0=5, n_period=3, device=torch_dev)
-    kc = counter(k, torch_dev)
-    out = {}
-    for thr in (9, 13):
-        monkeypatch.setenv("KF_BUCKET_MIN_K", str(thr))
-        c, t = kc.count(db)
-        torch.cuda.synchronize()
-        out[thr] = (c.clone(), t.clone())
-    assert torch.equal(out[9][0], out[13][0]) and torch.equal(out[9][1], out[13][1])
+    cnt, tot = counter(k, torch_dev).count(db)
+    torch.cuda.synchronize()
+    counts, totals = C.counts_to_numpy(cnt), tot.cpu().numpy()
+    host = db.data.cpu().numpy()
+    off = db.off.cpu().numpy()
+    for i in (0, 13, 39):
+        c, t = oracle.count(host[off[i]: off[i + 1]].tobytes(), k)
+        assert int(totals[i]) == t and (counts[i] == c).all(), i
+    assert int(totals.sum()) == int(counts.astype(np.uint64).sum())
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 8, 9])
-@pytest.mark.parametrize("k", [3, 5, 7, 8])
-def test_count_kernel_variants_match_oracle(torch_dev, oracle, monkeypatch, variant, k):
-    """The other shapes of the count kernel (KF_COUNT_VARIANT: 512-thread, the
-    1024-thread forward histogram K1 that k=7 used before K1w, 6-deep prefetch ring,
-    dynamic-chunk kernels with 4- and 6-deep rings) on ragged FASTA."""
-    monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
-    rng = np.random.default_rng(300 + 10 * variant + k)
+@pytest.mark.parametrize("k", [3, 5, 6, 7, 8])
+def test_ragged_fasta_medium_genomes(torch_dev, oracle, k):
+    """K1 (k <= 6) and K1x (k = 7, 8) on ragged multi-record FASTA of up to
+    200 kbp: records, N runs, lowercase, CRLF."""
+    rng = np.random.default_rng(300 + k)
     blobs = [gen.random_fasta(rng, int(rng.integers(0, 200000)), max_records=5, n_rate=0.002, lower=0.05,
                               crlf_rate=0.05) for _ in range(20)]
     counts, totals = run_batch(blobs, k, torch_dev)
-    check_against_oracle(oracle, blobs, k, counts, totals, tag=f"v{variant}")
+    check_against_oracle(oracle, blobs, k, counts, totals, tag=f"ragged-k{k}")
 
 
 def test_stream_probe_xor_fold(torch_dev):
@@ -390,15 +389,11 @@ def test_arbitrary_byte_values(torch_dev, oracle, k):
     check_against_oracle(oracle, blobs, k, counts, totals, fmt=1, tag="bytes")
 
 
-@pytest.mark.parametrize("variant", [5, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23])
-def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, variant):
-    """k=7 pair kernels (5: self-contained chunks, 10: static wave ranges, 12/13:
-    32-byte lanes): their
-    u16 LDS counters overflow on low-complexity sequence unless the drain path
-    moves counts out exactly (poly-A, dinucleotide and satellite repeats, N-broken
-    poly-A that fills the unpaired-window table, and FASTA lines of 1-7 bases that
-    keep every chunk on the irregular path)."""
-    monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
+def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle):
+    """k=7 K1x: its u16 LDS counters overflow on low-complexity sequence unless the
+    drain path moves counts out exactly (poly-A, dinucleotide and satellite
+    repeats, N-broken poly-A that fills the unpaired-window table, and FASTA lines
+    of 1-7 bases that keep every iteration on the irregular path)."""
     rng = np.random.default_rng(4242)
     sat = gen.random_seq(rng, 171).tobytes()
     polya = b"A" * 40_000_000
@@ -419,49 +414,14 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, monkeypatch, 
     check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16-many")
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23])
-def test_k7_kernel_variants_agree(torch_dev, oracle, monkeypatch, variant):
-    """k=7 pair kernels (KF_COUNT_VARIANT 5, 6, 7: self-contained chunks, prefetch
-    ring 6 / 4 / 8; 10, 11: static wave ranges, ring 6 / 8; 12, 13: 32-byte lanes,
-    ring 2 / 3) on ragged FASTA, like
-    the default forward-histogram kernel."""
-    monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
-    rng = np.random.default_rng(500 + variant)
-    blobs = [gen.random_fasta(rng, int(rng.integers(0, 300000)), max_records=5, n_rate=0.002, lower=0.05,
-                              crlf_rate=0.05, poly_rate=0.01) for _ in range(20)]
-    counts, totals = run_batch(blobs, 7, torch_dev)
-    check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"v{variant}")
-
-
-@pytest.mark.parametrize("variant", [19, 20, 22, 23])
-def test_k7_many_pieces_many_records(torch_dev, oracle, monkeypatch, variant):
+def test_k7_many_pieces_many_records(torch_dev, oracle):
     """Several genome pieces per workgroup, each with many records (excluded
     intervals), N runs and empty genomes."""
-    monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
-    rng = np.random.default_rng(2026 + variant)
+    rng = np.random.default_rng(2026 + 19)
     blobs = [gen.random_fasta(rng, int(rng.integers(0, 40000)) if i % 37 else 0, max_records=40, n_rate=0.003,
                               lower=0.05, crlf_rate=0.02, poly_rate=0.01) for i in range(700)]
     counts, totals = run_batch(blobs, 7, torch_dev)
-    check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"pieces-v{variant}")
-
-
-@pytest.mark.parametrize("frac,unit", [("0", "1"), ("0.5", "3"), ("1", "2"), ("0.85", "2"), ("0.9", "64")])
-def test_k7_claimed_units(torch_dev, oracle, monkeypatch, frac, unit):
-    """Variant 22 (K1x whose waves claim the last part of each piece in units
-    from a per-workgroup ticket): every static/claimed split, unit sizes from one
-    3 KiB iteration to 64, low-complexity genomes whose u16 drains happen inside
-    claimed units, and repeated launches (the tickets continue across launches)."""
-    monkeypatch.setenv("KF_COUNT_VARIANT", "22")
-    monkeypatch.setenv("KF_DYN_FRAC", frac)
-    monkeypatch.setenv("KF_DYN_UNIT", unit)
-    rng = np.random.default_rng(777 + int(float(frac) * 100) + int(unit))
-    blobs = [gen.random_fasta(rng, int(rng.integers(0, 1_500_000)), max_records=4, n_rate=0.002, lower=0.05,
-                              crlf_rate=0.02, poly_rate=0.01) for _ in range(24)]
-    blobs.append(b">polyA\n" + gen.wrap(np.frombuffer(b"A" * 6_000_000, np.uint8), 80))
-    blobs.append(b">ac\n" + gen.wrap(np.frombuffer(b"AC" * 2_000_000, np.uint8), 61))
-    for rep in range(2):
-        counts, totals = run_batch(blobs, 7, torch_dev)
-        check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"claim-{frac}-{unit}-{rep}")
+    check_against_oracle(oracle, blobs, 7, counts, totals, tag="pieces")
 
 
 def _k1x_wave_ranges(total, grid, wts=(20, 17, 11, 6)):
@@ -488,17 +448,12 @@ def _k1x_wave_ranges(total, grid, wts=(20, 17, 11, 6)):
     return out
 
 
-@pytest.mark.parametrize("variant", [18, 19, 21, 22, 23, pytest.param(20, marks=pytest.mark.xfail(
-    reason="variant 20 checks returns every other iteration: a counter grown only in unchecked iterations "
-           "passes 0xFFFF (why 19 is the default)", strict=True))])
-def test_k7_unchecked_iterations_adversarial(torch_dev, oracle, monkeypatch, variant):
-    """An input built against K1x's alternating return checks (variant 20: the
-    adds of every other 3 KiB iteration are not checked): every wave's odd
-    (unchecked) iterations are poly-A and its even ones hold no A at all, so no
-    checked add ever sees the AAAAAAAA counter, which alone would pass 0xFFFF
-    within one workgroup's piece.  The counts must still be exact."""
-    monkeypatch.setenv("KF_COUNT_VARIANT", str(variant))
-    monkeypatch.delenv("KF_WAVE_WEIGHTS", raising=False)
+def test_k7_unchecked_iterations_adversarial(torch_dev, oracle):
+    """An input built against return checks that skip iterations (the rejected
+    variant 20 of tools/zoo, which checked every other 3 KiB iteration, returned
+    574,653 for AAAAAAA here instead of 34,128,829): every wave's odd iterations
+    are poly-A and its even ones hold no A at all.  K1x checks every add's return,
+    so the counts must be exact."""
     rng = np.random.default_rng(99)
     L = 80_000_000
     head = b">adv\n"
@@ -517,29 +472,14 @@ def test_k7_unchecked_iterations_adversarial(torch_dev, oracle, monkeypatch, var
     arr[pos[(pos - len(head)) % 81 == 80]] = 10
     blobs = [arr.tobytes()]
     counts, totals = run_batch(blobs, 7, torch_dev)
-    check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"adv-v{variant}")
+    check_against_oracle(oracle, blobs, 7, counts, totals, tag="adv")
 
 
-def test_k7_stealing_repeated_launches(torch_dev, oracle, monkeypatch):
-    """Variant 23 (waves claim their own iterations from the front while idle
-    waves take back halves): genomes of every size class in one batch, several
-    launches in a row (the range words persist between launches, tagged by piece)."""
-    monkeypatch.setenv("KF_COUNT_VARIANT", "23")
-    rng = np.random.default_rng(2323)
-    blobs = [gen.random_fasta(rng, int(rng.choice([0, 100, 5000, 300_000, 3_000_000])), max_records=6, n_rate=0.002,
-                              lower=0.05, crlf_rate=0.01, poly_rate=0.01) for _ in range(40)]
-    blobs.append(b">polyA\n" + gen.wrap(np.frombuffer(b"A" * 8_000_000, np.uint8), 80))
-    for rep in range(3):
-        counts, totals = run_batch(blobs, 7, torch_dev)
-        check_against_oracle(oracle, blobs, 7, counts, totals, tag=f"steal-{rep}")
-
-
-def test_k8_single_pass_kernel(torch_dev, oracle, monkeypatch):
-    """Variant 24: k = 8 on the K1x front end (every window an 8-mer in u16 LDS
+def test_k8_single_pass_kernel(torch_dev, oracle):
+    """K1x8: k = 8 on the K1x front end (every window an 8-mer in u16 LDS
     counters, one pass): ragged FASTA with records, N runs, lowercase and CRLF;
     low-complexity genomes whose u16 halves drain (poly-A, dinucleotide, an
     8-mer palindrome repeat); many genome pieces per workgroup."""
-    monkeypatch.setenv("KF_COUNT_VARIANT", "24")
     rng = np.random.default_rng(8088)
     blobs = [gen.random_fasta(rng, int(rng.integers(0, 400_000)), max_records=5, n_rate=0.002, lower=0.05,
                               crlf_rate=0.05, poly_rate=0.01) for _ in range(24)]
@@ -651,3 +591,64 @@ def test_cli_64_bacterial_like_genomes(torch_dev, oracle, tmp_path):
     with ThreadPoolExecutor(8) as ex:
         bad = [nm for nm, ok in ex.map(check, blobs.items()) if not ok]
     assert not bad, bad
+
+
+def _chunk_genome(rng, n_contigs):
+    """Multi-contig FASTA that exercises get_chunks' pre-pass: N / n / '|' runs
+    (collapsed), gap letters "- \\t." (dropped; they split N runs), CRLF lines,
+    blank lines, lowercase, contigs around the 10 kbp threshold."""
+    out = []
+    for c in range(n_contigs):
+        L = int(rng.choice([3000, 9999, 10000, 10001, 15000, 24000, 61000]))
+        seq = gen.random_seq(rng, L, lower=0.02).copy()
+        for _ in range(int(rng.integers(0, 12))):
+            a = int(rng.integers(0, max(1, L - 300)))
+            seq[a: a + int(rng.integers(1, 300))] = np.frombuffer(b"NNnn|N", np.uint8)[rng.integers(0, 6)]
+        for _ in range(int(rng.integers(0, 20))):
+            seq[int(rng.integers(0, L))] = np.frombuffer(b"- \t.", np.uint8)[rng.integers(0, 4)]
+        body = gen.wrap(seq, int(rng.choice([60, 70, 80, 1000])), crlf=bool(rng.random() < 0.3))
+        if rng.random() < 0.2:
+            body = body.replace(b"\n", b"\n\n", 3)
+        out.append(b">ctg%d some description\n" % c + body)
+    return b"".join(out)
+
+
+def test_chunk_compact_matches_oracle(torch_dev, oracle):
+    """kf_chunk_compact (device linearise + N-run collapse + gap removal) == the
+    oracle's restatement of seqtk seq -l 0 | awk gsub | seqkit seq -g, record by
+    record, and every window of get_chunks' plan counts like the oracle."""
+    from kf2vecfsw_amd import chunks as CH
+    rng = np.random.default_rng(4040)
+    for t in range(6):
+        data = _chunk_genome(rng, int(rng.integers(1, 12)))
+        names, starts, d_seq = CH.ChunkPipeline(counter(7, torch_dev), torch_dev, 16, 2).windows_of(data, "s")
+        exp = oracle.chunk_windows(data, "s")
+        assert names == [n for n, _ in exp]
+        got = d_seq.cpu().numpy()
+        for st, (_, w) in zip(starts, exp):
+            assert got[int(st): int(st) + 10000].tobytes() == w
+
+
+def test_cli_get_chunks_multicontig_vs_oracle(torch_dev, oracle, tmp_path):
+    """get_chunks CLI on several multi-contig genomes (one device batch, then a
+    batch smaller than a genome's windows): every row == the oracle's window
+    counts (raw), in the oracle's order; genomes with < 5 windows are excluded."""
+    from kf2vecfsw_amd import main as M
+    rng = np.random.default_rng(5050)
+    inp = tmp_path / "in"
+    inp.mkdir()
+    genomes = {f"g{i}": _chunk_genome(rng, int(rng.integers(1, 9))) for i in range(7)}
+    for name, b in genomes.items():
+        (inp / f"{name}.fna").write_bytes(b)
+    for batch_gb in ("1", "0.00005"):   # 0.00005 GiB ~ 5 windows: flushes inside and across genomes
+        out = tmp_path / f"out{batch_gb}"
+        out.mkdir()
+        M.main(["get_chunks", "-input_dir", str(inp), "-output_dir", str(out), "-k", "7", "-batch_gb", batch_gb])
+        for name, b in genomes.items():
+            wins = oracle.chunk_windows(b, name)
+            f = out / f"{name}.kf"
+            if len(wins) < 5:
+                assert not f.exists(), name
+                continue
+            exp = "".join(oracle.kf_line(n, oracle.count(b">w\n" + w + b"\n", 7)[0], raw_cnt=True) for n, w in wins)
+            assert f.read_text() == exp, name

@@ -137,19 +137,27 @@ def test_count_batch_rejects_bad_args(native):
     assert L.kf_count_batch(None, None, 0, None, 0, None, None, 7, None, None, 0, None) == N.KF_OK
 
 
-def test_chunk_window_plan_matches_oracle(oracle):
-    """Host window plan of get_chunks (product) == oracle restatement, on the toy genomes."""
+def test_chunk_window_plan_counts():
+    """get_chunks window plan (main.py:813-818 + seqkit sliding's whole windows):
+    the number of windows for contig lengths around the 10 kbp boundaries."""
     from kf2vecfsw_amd import chunks as CH
-    for f in sorted(os.listdir(os.path.join(TOY, "train_tree_fna"))):
-        data = gzip.open(os.path.join(TOY, "train_tree_fna", f)).read()
-        sample = f[:-3].rsplit(".f", 1)[0]
-        a = CH.genome_windows(data, sample)
-        b = oracle.chunk_windows(data, sample)
-        assert [x[0] for x in a] == [x[0] for x in b]
-        assert all(x[1] == y[1] for x, y in zip(a, b))
     for L in [9999, 10000, 10001, 19999, 20000, 25000, 1241422]:
         n, step = CH.window_plan(L)
         assert n == (0 if L < 10000 else len(range(0, L - 10000 + 1, step)))
+        if n:
+            assert (n - 1) * step + 10000 <= L and 0 < step <= 10000
+
+
+def test_chunk_record_regions(native):
+    """Sequence regions after each header line and the contig ids (first word,
+    trailing CR dropped) that name the windows."""
+    import numpy as np
+    from kf2vecfsw_amd import chunks as CH
+    data = np.frombuffer(b"junk\n>c1 desc\r\nACGT\nAC\n>c2\nGG\n>\n\n>c4 x", np.uint8)
+    se, ids = CH.record_regions(data)
+    assert ids == ["c1", "c2", "", "c4"]
+    regs = [data[int(se[2 * i]): int(se[2 * i + 1])].tobytes() for i in range(len(ids))]
+    assert regs == [b"ACGT\nAC\n", b"GG\n", b"\n", b""]
 
 
 def test_get_kmers_matrix_matches_reference_restatement(native, oracle):

@@ -28,7 +28,7 @@
 #include <mutex>
 #include <vector>
 
-#include "kf_front.h"
+#include "kf_front_zoo.h"
 #include "kf_internal.h"
 
 namespace kf {
@@ -96,17 +96,6 @@ __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
 }
 __device__ __forceinline__ uint32_t lds_xchg(uint32_t a, uint32_t v) {
     return __hip_atomic_exchange((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Byte address (x 4) of the record in u16 half h of d: one SDWA shift.
-__device__ __forceinline__ uint32_t rec_addr(uint32_t d, int h) {
-    uint32_t r;
-    if (h == 0)
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
-            : "=v"(r) : "v"(d));
-    else
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
-            : "=v"(r) : "v"(d));
-    return r;
 }
 __device__ __forceinline__ uint32_t lds_ld(uint32_t a) { return *(volatile lds_u32*)(uintptr_t)a; }
 __device__ __forceinline__ void lds_st(uint32_t a, uint32_t v) { *(volatile lds_u32*)(uintptr_t)a = v; }
@@ -178,35 +167,6 @@ __device__ __forceinline__ void canon_std(const Windows& w, uint32_t (&s)[16]) {
         const uint32_t c = __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, W2);
         s[r] = ((w.R >> r) & 1u) ? min(f, c) : 0xFFFFFFFFu;
     }
-}
-
-// Window register of a 1 KiB chunk in the fast case (uniform): every lane's 16
-// bytes are bases with at most one newline and the carry is complete (>= k-1
-// bases).  Then the context is lane L-1's raw codes and no validity mask, tail
-// or run mask is needed: windows 0..ne-1 are valid (ne = 15 or 16).  Returns
-// false (w untouched) otherwise; the caller takes the general path.
-template <int K>
-__device__ __forceinline__ bool fast_windows(const uint4 d, uint32_t carry, Windows& w) {
-    constexpr uint32_t TM = (1u << (2 * (K - 1))) - 1u;
-    static_assert(K - 1 <= 11, "the carry holds 11 entries");
-    uint32_t Cf, NNL, bad;
-    classify16_fast(d, Cf, NNL, bad);
-    const uint32_t nef = (uint32_t)__builtin_popcount(NNL);
-    const bool self_ok = bad == 0 && nef >= 15u;
-    carry = __builtin_amdgcn_readfirstlane(carry);
-    if (t_n(carry) < (uint32_t)(K - 1) || __builtin_amdgcn_ballot_w64(!self_ok) != 0) return false;
-    // drop the newline entry (none: r = 16, identity)
-    const uint32_t r = (uint32_t)__builtin_ctz((NNL ^ 0xFFFFu) | 0x10000u);
-    const uint32_t lo1 = (1u << r) - 1u, lo2 = lo1 | (lo1 << r);
-    const uint32_t C = bfi(lo2, Cf, Cf >> 2);
-    const uint32_t pC = wave_shr1(t_codes(carry), C);
-    const uint64_t W = ((uint64_t)pC << (2u * nef)) | (uint64_t)C;
-    w.wlo = (uint32_t)W;
-    w.whi = (uint32_t)(W >> 32);
-    w.R = (1u << nef) - 1u;
-    // lane 63's block is all valid bases: its tail is complete
-    w.next = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)C, kWave - 1) & TM, 31u, 31u);
-    return true;
 }
 
 template <int K>
@@ -281,35 +241,21 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             for (uint32_t b = tid; b < NBK; b += kBkBlock) lds_st(cz + 4 * b, 0u);
             uint32_t s[16], rk[16];
             const bool have = r < nch;
-            bool dense = false;   // wave-uniform: windows 0..14 of every lane are valid (fast case)
             if (have) {
                 Windows w;
-                const bool msk = rg.masked(A, rel);
-                if (!msk && fast_windows<K>(bf, carry, w)) {
-                    // every lane's 16 bytes are bases with at most one newline and
-                    // the carry is complete: windows 0..14 valid, 15 unless a
-                    // newline; ranks without per-record branches
-                    dense = true;
-                    carry = w.next;
-                    canon_std<K>(w, s);
-#pragma unroll
-                    for (int j = 0; j < 15; ++j) rk[j] = lds_add_rtn(cb + ((s[j] >> kBkBits) << 2), 1u);
-                    if (s[15] != 0xFFFFFFFFu) rk[15] = lds_add_rtn(cb + ((s[15] >> kBkBits) << 2), 1u);
+                uint32_t C, V, EN, ne, own;
+                if (rg.masked(A, rel)) {
+                    front_end<K, true, false>(bf, A, rg.c0 + rel, lane, rg.mask(), rg.iv, C, V, EN, ne, own);
+                    w = windows<K, true>(C, V, EN, ne, carry, lane);
                 } else {
-                    uint32_t C, V, EN, ne, own;
-                    if (msk) {
-                        front_end<K, true, false>(bf, A, rg.c0 + rel, lane, rg.mask(), rg.iv, C, V, EN, ne, own);
-                        w = windows<K, true>(C, V, EN, ne, carry, lane);
-                    } else {
-                        front_end<K, false, false>(bf, A, rg.c0 + rel, lane, rg.mask(), rg.iv, C, V, EN, ne, own);
-                        w = windows<K, false>(C, V, EN, ne, carry, lane);
-                    }
-                    carry = w.next;
-                    canon_std<K>(w, s);
-#pragma unroll
-                    for (int j = 0; j < 16; ++j)
-                        if (s[j] != 0xFFFFFFFFu) rk[j] = lds_add_rtn(cb + ((s[j] >> kBkBits) << 2), 1u);
+                    front_end<K, false, false>(bf, A, rg.c0 + rel, lane, rg.mask(), rg.iv, C, V, EN, ne, own);
+                    w = windows<K, false>(C, V, EN, ne, carry, lane);
                 }
+                carry = w.next;
+                canon_std<K>(w, s);
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (s[j] != 0xFFFFFFFFu) rk[j] = lds_add_rtn(cb + ((s[j] >> kBkBits) << 2), 1u);
                 rel += kChunk;
                 if (rel + 3 * kChunk < nch * kChunk) bf = rg.load(A.bytes, rel + 3 * kChunk, lane);
             }
@@ -363,17 +309,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                             *(volatile lds_u16*)(uintptr_t)(st + 2 * (e + x)) = (uint16_t)(kSentinel | ((e + x) & 63u));
                 }
             }
-            if (dense) {
-#pragma unroll
-                for (int j = 0; j < 15; ++j) {
-                    const uint32_t slot = lds_ld(rb + ((s[j] >> kBkBits) << 2)) + rk[j];
-                    *(volatile lds_u16*)(uintptr_t)(st + 2 * slot) = (uint16_t)(s[j] & (kBkCodes - 1));
-                }
-                if (s[15] != 0xFFFFFFFFu) {
-                    const uint32_t slot = lds_ld(rb + ((s[15] >> kBkBits) << 2)) + rk[15];
-                    *(volatile lds_u16*)(uintptr_t)(st + 2 * slot) = (uint16_t)(s[15] & (kBkCodes - 1));
-                }
-            } else if (have) {
+            if (have) {
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     if (s[j] != 0xFFFFFFFFu) {
@@ -496,7 +432,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                 if (G.act & (1u << x)) {
                     const uint32_t d[4] = {G.v[x].x, G.v[x].y, G.v[x].z, G.v[x].w};
 #pragma unroll
-                    for (int t = 0; t < 8; ++t) lds_add(rec_addr(d[t >> 1], t & 1), 1u);
+                    for (int t = 0; t < 8; ++t) lds_add(((d[t >> 1] >> (16 * (t & 1))) & 0xFFFFu) << 2, 1u);
                 }
             }
         };
@@ -655,9 +591,6 @@ uint32_t bucket_lds_for(int k) {
 // that could give a wave more than 64 runs of a piece is refused (default used).
 uint32_t bucket_weights() {
     constexpr uint32_t kDefault = 0x01010101u;
-#ifndef KF_PROFILE_BUILD
-    return kDefault;   // the knob is read in profiling builds only
-#endif
     const char* e = getenv("KF_BK_WEIGHTS");
     if (!e || !*e) return kDefault;
     unsigned a[4];
@@ -792,11 +725,7 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     B.accumulate = (flags & KF_ACCUMULATE) ? 1u : 0u;
     B.slot_w = bucket_weights();
     B.prof = nullptr;
-#ifdef KF_PROFILE_BUILD
     const char* pe = getenv("KF_BUCKET_PROFILE");   // debugging aid: synchronous, prints to stderr
-#else
-    const char* pe = nullptr;   // (kf_count_batch stays asynchronous and allocation-free per launch)
-#endif
     std::vector<unsigned long long> prof_h;
     if (pe && *pe == '1') {
         if (hipMalloc((void**)&B.prof, (size_t)grid * (8 + 4 * kBkWaves) * 8) != hipSuccess ||

@@ -22,8 +22,16 @@ struct CountArgs {
     unsigned long long* totals;
     uint32_t nbins;
     int32_t n_genomes;
+    unsigned long long* prof;      // optional cycle counters (KF_COUNT_PROFILE=1), else null
+    uint32_t wave_w;               // K1x: share of a genome piece by wave slot (4 x 8 bit, see split_at_w)
     uint32_t flags;                // kf_count_batch flags (KF_ACCUMULATE)
+    // K1x variant 22: the last part of each genome piece is claimed in units by
+    // the workgroup's waves (claim ticket per workgroup, kClaimStride apart)
+    uint32_t* claim;
+    uint32_t dyn_frac;             // statically split share of a piece, 2^-20 fixed point
+    uint32_t dyn_unit;             // bytes per claimed unit (a multiple of 3 KiB)
 };
+constexpr uint32_t kClaimStride = 32;   // u32 words between two workgroups' tickets (128 B)
 
 // ---------------------------------------------------------------- tails
 // A "tail" summarises a stretch of the compacted entry stream:
@@ -343,6 +351,14 @@ __device__ __forceinline__ uint32_t chunk_tail(const uint8_t* bytes, const uint6
 // at c0 + rel (rel = 0, 1024, ...).  Chunk bookkeeping is in 32-bit offsets from
 // c0 (a wave range is far below 4 GiB): gfx9 SALU has no 64-bit ordered
 // compare, so 64-bit bounds tests would run on the VALU once per chunk.
+// An excluded-interval cursor carried from one wave range to the next one of
+// the same wave at a later position (K1x variant 22): interval iv and its
+// absolute bounds; every interval before iv ends at or before the old position.
+struct IvHint {
+    uint64_t iv, s, e;
+    bool valid;
+};
+
 struct Range {
     uint64_t c0, glo, ghi, lo, hi;
     uint32_t lo_r, hi_r, end_r, nch;
@@ -390,8 +406,10 @@ struct Range {
     // case: they lie inside the genome, outside every excluded interval, and end
     // in >= k-1 bases); anything else takes warm.  Same carry as warm for every
     // use (codes of the last k-1 entries, a run of >= k-1).
+    // With a valid hint from an earlier position whose interval ends after p16,
+    // the search and the bounds' loads are skipped.
     template <int K>
-    __device__ __forceinline__ void warm16(const CountArgs& A, int lane) {
+    __device__ __forceinline__ void warm16(const CountArgs& A, int lane, const IvHint* hint = nullptr) {
         if (c0 < glo + 16) {   // the genome start is within reach
             warm<K>(A, lane);
             return;
@@ -399,10 +417,14 @@ struct Range {
         const uint64_t p16 = c0 - 16;
         const uint4 d = *(const uint4*)(A.bytes + p16);   // the same 16 bytes in every lane
         uint64_t s_iv = ~0ull, e_iv = ~0ull;
-        iv = wave_upper_bound(A.n_excl, p16, lane, [&](uint64_t i) { return A.excl[2 * i + 1]; });
-        if (iv < A.n_excl) {
-            s_iv = uload64(A.excl + 2 * iv);
-            e_iv = uload64(A.excl + 2 * iv + 1);
+        if (hint && hint->valid && hint->e > p16) {
+            iv = hint->iv, s_iv = hint->s, e_iv = hint->e;
+        } else {
+            iv = wave_upper_bound(A.n_excl, p16, lane, [&](uint64_t i) { return A.excl[2 * i + 1]; });
+            if (iv < A.n_excl) {
+                s_iv = uload64(A.excl + 2 * iv);
+                e_iv = uload64(A.excl + 2 * iv + 1);
+            }
         }
         uint32_t C, V, EN, ne, own;
         const ChunkMask m{glo, 0, 0};
@@ -416,6 +438,7 @@ struct Range {
         ive_r = iv < A.n_excl ? rel_of(e_iv) : 0xFFFFFFFFu;
         ivs_a = s_iv, ive_a = e_iv;
     }
+    __device__ __forceinline__ IvHint hint() const { return IvHint{iv, ivs_a, ive_a, true}; }
     // As warm, with the first chunk before c0 already loaded (ctx_load).
     template <int K>
     __device__ __forceinline__ void warm_from(const CountArgs& A, const uint4 dctx, int lane) {
