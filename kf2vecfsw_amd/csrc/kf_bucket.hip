@@ -33,11 +33,19 @@
 
 namespace kf {
 
-// Profiling-only ablations (tools/build_abl.sh -DKF_BK_ABL=n; counts are wrong):
-// 1 = no col_idx table reads in the flush, 2 = no record reads in phase 2
-// (hashed stand-ins).
+// Profiling-only ablations (-DKF_BK_ABL=n through KF_HIPCC_FLAGS; counts are
+// wrong): 1 = no col_idx table reads in the flush, 2 = no record reads in phase
+// 2 (hashed stand-ins), 3 = no phase-1 rank atomics (dense path), 4 = no
+// phase-1 staging writes (dense path), 5 = no phase-2 histogram adds, 7 = rank
+// adds without returns.
 #ifndef KF_BK_ABL
 #define KF_BK_ABL 0
+#endif
+// Phase 2 record groups: 1 = two groups of 4 windows alternate (the next one in
+// flight while one is counted), 0 = one group of 8 windows (a bucket's further
+// groups wait for their loads).
+#ifndef KF_BK_DB
+#define KF_BK_DB 1
 #endif
 
 constexpr int kBkBits = 15;                          // 32768 codes per bucket
@@ -293,7 +301,16 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                     carry = w.next;
                     canon_std<K>(w, s);
 #pragma unroll
+#if KF_BK_ABL == 3   // profiling only: no rank atomics (ranks by lane: wrong counts)
+                    for (int j = 0; j < 15; ++j) rk[j] = (uint32_t)lane * 16 + j;
+#elif KF_BK_ABL == 7   // profiling only: rank adds without returns (ranks by lane: wrong counts)
+                    for (int j = 0; j < 15; ++j) {
+                        lds_add(cb + ((s[j] >> kBkBits) << 2), 1u);
+                        rk[j] = (uint32_t)lane * 16 + j;
+                    }
+#else
                     for (int j = 0; j < 15; ++j) rk[j] = lds_add_rtn(cb + ((s[j] >> kBkBits) << 2), 1u);
+#endif
                     if (s[15] != 0xFFFFFFFFu) rk[15] = lds_add_rtn(cb + ((s[15] >> kBkBits) << 2), 1u);
                 } else {
                     uint32_t C, V, EN, ne, own;
@@ -367,7 +384,11 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
 #pragma unroll
                 for (int j = 0; j < 15; ++j) {
                     const uint32_t slot = lds_ld(rb + ((s[j] >> kBkBits) << 2)) + rk[j];
+#if KF_BK_ABL == 4   // profiling only: no staging writes (wrong counts)
+                    asm volatile("" ::"v"(slot), "v"(s[j]));
+#else
                     *(volatile lds_u16*)(uintptr_t)(st + 2 * slot) = (uint16_t)(s[j] & (kBkCodes - 1));
+#endif
                 }
                 if (s[15] != 0xFFFFFFFFu) {
                     const uint32_t slot = lds_ld(rb + ((s[15] >> kBkBits) << 2)) + rk[15];
@@ -455,7 +476,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             t.w0 = 0;
             return t;
         };
-        constexpr int kGW = 8;
+        constexpr int kGW = KF_BK_DB ? 4 : 8;
         struct Grp {
             v4u v[kGW];
             uint32_t act;   // bit x: this lane's unit of window x exists
@@ -495,8 +516,12 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                 if (G.w0 + x * kWave >= U) break;   // wave-uniform
                 if (G.act & (1u << x)) {
                     const uint32_t d[4] = {G.v[x].x, G.v[x].y, G.v[x].z, G.v[x].w};
+#if KF_BK_ABL == 5   // profiling only: phase 2 without its histogram adds (wrong counts)
+                    asm volatile("" ::"v"(d[0]), "v"(d[1]), "v"(d[2]), "v"(d[3]));
+#else
 #pragma unroll
                     for (int t = 0; t < 8; ++t) lds_add(rec_addr(d[t >> 1], t & 1), 1u);
+#endif
                 }
             }
         };
@@ -560,16 +585,34 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         uint32_t re_cur = re_next;
         re_next = meta_at(NBK > 1 ? 2 : 1);
         Grp G0;
+#if KF_BK_DB
+        Grp G1;
+#endif
         issue(tb, G0);
         uint64_t tp[4] = {0, 0, 0, 0};   // profile: records, barrier, flush, barrier
         uint64_t tcons = 0;              // profile: consume part of records
         for (uint32_t b = 0; b < NBK; ++b) {
             uint64_t t0 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
+#if KF_BK_DB
+            // two groups alternate: the bucket's next group is always in flight
+            // while one is counted (issued unconditionally -- past the bucket's
+            // end its lanes are inactive and read unit 0 -- so the compiler's
+            // vmcnt stays exact: wait for the consumed group only)
+            for (;;) {
+                issue(tb, G1);
+                consume(G0, tb.U);
+                if (G1.w0 >= tb.U) break;
+                issue(tb, G0);
+                consume(G1, tb.U);
+                if (G0.w0 >= tb.U) break;
+            }
+#else
             consume(G0, tb.U);
             while (tb.w0 < tb.U) {   // a bucket beyond one group: synchronous groups
                 issue(tb, G0);
                 consume(G0, tb.U);
             }
+#endif
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tcons += __builtin_amdgcn_s_memtime() - t0; }
             v2u ci[kFG];
             // issue order: bucket b+2's run ends, the flush's col_idx, bucket

@@ -652,3 +652,29 @@ def test_cli_get_chunks_multicontig_vs_oracle(torch_dev, oracle, tmp_path):
                 continue
             exp = "".join(oracle.kf_line(n, oracle.count(b">w\n" + w + b"\n", 7)[0], raw_cnt=True) for n, w in wins)
             assert f.read_text() == exp, name
+
+
+def test_features_handoff_equals_kf_text_round_trip(torch_dev, toy, tmp_path):
+    """counter.features on the device count matrix == what the
+    trainers compute from the `.kf` files (utils.my_read_csv = pd.read_csv(...,
+    index_col=0, header=None), then * features_scaler 1e4,
+    train_classifier_model.py:144-150), bit for bit, in all four output modes."""
+    import pandas as pd
+    import torch
+    from kf2vecfsw_amd import counter as C
+    from kf2vecfsw_amd import main as M
+    blobs = [t[2] for t in toy] + [b"", b">t\nACGTACGTTTGA\n"]
+    names = [t[1] for t in toy] + ["empty", "tiny"]
+    counts, _ = counter(7, torch_dev).count(C.to_device(C.pack_genomes(blobs, names), torch_dev))
+    host = C.counts_to_numpy(counts)
+    for pseudo in (False, True):
+        for raw in (False, True):
+            X = C.features(counts, pseudocount=pseudo, raw_cnt=raw, scaler=1e4).cpu().numpy()
+            for i, name in enumerate(names):
+                f = tmp_path / f"{name}_{pseudo:d}{raw:d}.kf"
+                f.write_bytes(M.format_kf(name, host[i], pseudo, raw))
+                ref = pd.read_csv(f, index_col=0, header=None, sep=",").values.astype(np.float64)[0] * 1e4
+                assert np.array_equal(np.isnan(ref), np.isnan(X[i])), (name, pseudo, raw)
+                ok = ~np.isnan(ref)
+                assert np.array_equal(ref[ok], X[i][ok]), (name, pseudo, raw)
+    torch.cuda.synchronize()
