@@ -251,11 +251,14 @@ def features(counts: torch.Tensor, pseudocount: bool = False, raw_cnt: bool = Fa
     `* features_scaler` (train_classifier_model.py:148, train_model_set.py:291) --
     computed on the device from the count matrix, without the text round trip.
 
-    Bit-identical to parsing the `.kf` text: the values are main.py:332-342
-    (`+0.5` pseudocount, `v / v.sum()` unless raw) in float64; the row sums are
-    exact (integers or halves below 2^53), each quotient is correctly rounded,
-    and `repr` text round-trips float64 exactly.  An empty genome gives NaN
-    rows, as the reference's "nan" strings parse.
+    The values are main.py:332-342 (`+0.5` pseudocount, `v / v.sum()` unless raw)
+    in float64: the row sums are exact (integers or halves below 2^53) and each
+    quotient is correctly rounded, so they equal the numbers the `.kf` text holds
+    (`repr` round-trips float64; `pd.read_csv(..., float_precision="round_trip")`
+    reads them back bit for bit).  pandas' default parser, which my_read_csv
+    uses, is not correctly rounded: it lands within 1 ulp of these values (about
+    two thirds of the entries of a k=7 row differ in the last bit).  An empty
+    genome gives NaN rows (normalised) as the reference's "nan" strings parse.
     """
     c = counts.to(torch.int64)
     c = torch.where(c < 0, c + (1 << 32), c)          # uint32 bit patterns held in int32

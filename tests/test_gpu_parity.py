@@ -655,10 +655,11 @@ def test_cli_get_chunks_multicontig_vs_oracle(torch_dev, oracle, tmp_path):
 
 
 def test_features_handoff_equals_kf_text_round_trip(torch_dev, toy, tmp_path):
-    """counter.features on the device count matrix == what the
-    trainers compute from the `.kf` files (utils.my_read_csv = pd.read_csv(...,
-    index_col=0, header=None), then * features_scaler 1e4,
-    train_classifier_model.py:144-150), bit for bit, in all four output modes."""
+    """counter.features on the device count matrix == the float64
+    values the `.kf` text holds (pd.read_csv(..., float_precision="round_trip"),
+    x features_scaler 1e4), bit for bit, in all four output modes.  The
+    trainers' own reader (utils.my_read_csv: pandas' default parser, which is not
+    correctly rounded) lands within 1 ulp of them before the scaling."""
     import pandas as pd
     import torch
     from kf2vecfsw_amd import counter as C
@@ -670,11 +671,15 @@ def test_features_handoff_equals_kf_text_round_trip(torch_dev, toy, tmp_path):
     for pseudo in (False, True):
         for raw in (False, True):
             X = C.features(counts, pseudocount=pseudo, raw_cnt=raw, scaler=1e4).cpu().numpy()
+            X1 = C.features(counts, pseudocount=pseudo, raw_cnt=raw).cpu().numpy()
             for i, name in enumerate(names):
                 f = tmp_path / f"{name}_{pseudo:d}{raw:d}.kf"
                 f.write_bytes(M.format_kf(name, host[i], pseudo, raw))
-                ref = pd.read_csv(f, index_col=0, header=None, sep=",").values.astype(np.float64)[0] * 1e4
-                assert np.array_equal(np.isnan(ref), np.isnan(X[i])), (name, pseudo, raw)
-                ok = ~np.isnan(ref)
-                assert np.array_equal(ref[ok], X[i][ok]), (name, pseudo, raw)
+                exact = pd.read_csv(f, index_col=0, header=None, sep=",",
+                                    float_precision="round_trip").values.astype(np.float64)[0]
+                assert np.array_equal(np.isnan(exact), np.isnan(X[i])), (name, pseudo, raw)
+                ok = ~np.isnan(exact)
+                assert np.array_equal(exact[ok] * 1e4, X[i][ok]), (name, pseudo, raw)
+                dflt = pd.read_csv(f, index_col=0, header=None, sep=",").values.astype(np.float64)[0]
+                assert np.all(np.abs(dflt[ok] - X1[i][ok]) <= np.spacing(np.abs(X1[i][ok]))), (name, pseudo, raw)
     torch.cuda.synchronize()

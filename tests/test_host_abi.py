@@ -182,7 +182,9 @@ def test_get_kmers_matrix_matches_reference_restatement(native, oracle):
 @pytest.mark.parametrize("raw", [False, True])
 def test_features_handoff_equals_kf_text_round_trip(native, pseudo, raw):
     """counter.features (in-memory hand-off) == parsing the `.kf` line the writer
-    produces, times the trainers' scaler: bit for bit (CPU torch)."""
+    produces, times the trainers' scaler: bit for bit (CPU torch).  Python's
+    float() is correctly rounded, like pandas' float_precision="round_trip"; the
+    GPU twin also bounds pandas' default parser (<= 1 ulp)."""
     import torch
     from kf2vecfsw_amd import counter as C
     from kf2vecfsw_amd.main import format_kf
