@@ -256,8 +256,8 @@ def features(counts: torch.Tensor, pseudocount: bool = False, raw_cnt: bool = Fa
     quotient is correctly rounded, so they equal the numbers the `.kf` text holds
     (`repr` round-trips float64; `pd.read_csv(..., float_precision="round_trip")`
     reads them back bit for bit).  pandas' default parser, which my_read_csv
-    uses, is not correctly rounded: it lands within 1 ulp of these values (about
-    two thirds of the entries of a k=7 row differ in the last bit).  An empty
+    uses, is not correctly rounded: about half the entries of a k=7 row read
+    differently, by at most ~1e-12 relative (8.7e-13 measured on the toy genomes).  An empty
     genome gives NaN rows (normalised) as the reference's "nan" strings parse.
     """
     c = counts.to(torch.int64)
