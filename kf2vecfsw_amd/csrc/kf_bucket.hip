@@ -52,22 +52,10 @@ constexpr int kBkBits = 15;                          // 32768 codes per bucket
 constexpr uint32_t kBkCodes = 1u << kBkBits;
 constexpr int kBkWaves = 16;
 constexpr int kBkBlock = kBkWaves * kWave;
-// Phase 1 runs in two independent halves of 8 waves (waves 0-7 own the first
-// half of a piece, 8-15 the second), each with its own rounds, counters, staging
-// buffers and an LDS spin barrier, so the LDS-heavy rank step of one half
-// overlaps the VALU-heavy front end of the other instead of all 16 waves doing
-// the same step between workgroup barriers.
-constexpr int kBkHalves = 2;
-constexpr int kHalfWaves = kBkWaves / kBkHalves;
-constexpr int kHalfBlock = kHalfWaves * kWave;
-constexpr uint32_t kRoundRecs = kHalfWaves * kChunk;   // windows per half-round (<= 8192)
-// bytes per piece (one workgroup): a wave range is <= piece/16 + 16 bytes, so a
-// half has <= kRmax rounds and a bucket <= 2 kRmax = 996 runs, which phase 2
-// deals to 16 waves x 64 lanes
-constexpr uint64_t kPieceMax = (8ull << 20) - (256ull << 10);
-constexpr uint32_t kRmax = (uint32_t)(kPieceMax / kBkWaves / kChunk) + 2;   // rounds per half
-constexpr uint32_t kRuns = kBkHalves * kRmax;                               // run slots per bucket
-static_assert(kRuns <= (uint32_t)(kBkWaves * kWave), "phase 2 deals every run to one lane");
+constexpr uint32_t kRoundRecs = kBkWaves * kChunk;   // windows per round (<= 16384)
+constexpr uint64_t kPieceMax = 8ull << 20;           // bytes per piece (one workgroup)
+// rounds per piece: a wave range is <= piece/16 + 16 bytes, i.e. <= 513 chunks
+constexpr uint32_t kRmax = (uint32_t)(kPieceMax / kRoundRecs) + 2;
 // A record is s & 0x7FFF.  Runs (one bucket, one round) are padded to whole
 // 8-record units with sentinels 0x8000 | x, which phase 2 counts into a trash
 // area past the histogram, so a 16-byte unit never needs a range test.
@@ -76,28 +64,23 @@ constexpr uint32_t kSentinel = 0x8000u;
 template <int K>
 struct Bk {
     static constexpr uint32_t nbk = (1u << (2 * K)) >> kBkBits;   // buckets
-    static constexpr uint32_t round_cap = kRoundRecs + 7 * nbk;     // records of a padded half-round
-    static constexpr uint64_t rec_cap_half = (uint64_t)kRmax * round_cap + 8;
-    static constexpr uint64_t rec_cap = kBkHalves * rec_cap_half;  // per workgroup
+    static constexpr uint32_t round_cap = kRoundRecs + 7 * nbk;     // records of a padded round
+    static constexpr uint64_t rec_cap = (uint64_t)kRmax * round_cap + 8;   // per workgroup
     // LDS byte layout.  Phase 2: the 128 KiB histogram at 0.  Phase 1 reuses it:
-    // per half, two round staging buffers and one private bucket-offset table per
-    // wave.  After the histogram: per half three rotating sets of round rank
-    // counters (phase 1), which phase 2 reuses as the sentinels' trash bins, the
-    // two halves' barrier counters, and the reduction slots.
+    // two round staging buffers, then one private bucket-offset table per wave.
+    // After the histogram: three rotating sets of round rank counters (phase 1),
+    // which phase 2 reuses as the sentinels' trash bins, and the reduction slots.
     static constexpr uint32_t hist = 0;
     static constexpr uint32_t stage_bytes = (round_cap * 2 + 15) & ~15u;
-    static constexpr uint32_t half_bytes = (2 * stage_bytes + kHalfWaves * (nbk + 1) * 4 + 15) & ~15u;
-    static constexpr uint32_t dirty = kBkHalves * half_bytes;         // phase-1 footprint in hist
-    static constexpr uint32_t cnt = kBkCodes * 4;                   // + (3 h + r % 3) * nbk * 4
-    // (past the counters and past phase 2's 64 trash bins at cnt)
-    static constexpr uint32_t bar = cnt + (3 * kBkHalves * nbk * 4 > 256 ? 3 * kBkHalves * nbk * 4 : 256);   // + 4 h
-    static constexpr uint32_t red = (bar + 4 * kBkHalves + 7) & ~7u;   // kBkWaves u64
-    static constexpr uint32_t lds_bytes = red + kBkWaves * 8;
-    __device__ static constexpr uint32_t stage(uint32_t h, uint32_t r) { return h * half_bytes + (r & 1) * stage_bytes; }
-    __device__ static constexpr uint32_t rbase(uint32_t h) { return h * half_bytes + 2 * stage_bytes; }
+    static constexpr uint32_t stage = 0;                            // + (r & 1) * stage_bytes
+    static constexpr uint32_t rbase = 2 * stage_bytes;              // + wave * (nbk + 1) * 4
+    static constexpr uint32_t dirty = rbase + kBkWaves * (nbk + 1) * 4;   // phase-1 footprint in hist
+    static constexpr uint32_t cnt = kBkCodes * 4;                   // + (r % 3) * nbk * 4
+    static constexpr uint32_t red = (cnt + 3 * nbk * 4 + 7) & ~7u;  // kBkWaves u64
+    static constexpr uint32_t lds_bytes =
+        red + kBkWaves * 8 > cnt + 256 ? red + kBkWaves * 8 : cnt + 256;   // trash: 64 bins at cnt
     static_assert(dirty <= kBkCodes * 4, "phase-1 tables must fit the histogram area");
     static_assert(round_cap < 65536, "round offsets are u16");
-    static_assert(lds_bytes <= 160 * 1024, "LDS");
 };
 
 struct BucketArgs {
@@ -105,9 +88,10 @@ struct BucketArgs {
     const uint32_t* bcol;      // nbk+1: first column of each bucket
     const uint32_t* pstart;    // n_genomes+1: first piece of each genome
     uint16_t* rec;             // gridDim.x * Bk<K>::rec_cap records
-    uint16_t* meta;            // gridDim.x * (nbk+1) * kRuns run bucket offsets (run = h kRmax + round)
-    uint32_t* roff;            // gridDim.x * kRuns run record offsets
+    uint16_t* meta;            // gridDim.x * (nbk+1) * kRmax round bucket offsets
+    uint32_t* roff;            // gridDim.x * kRmax round record offsets
     uint32_t accumulate;
+    uint32_t slot_w;            // phase-2 rounds per wave by wave slot (4 x 8 bit, see bucket_weights)
     unsigned long long* prof;   // optional (KF_BUCKET_PROFILE): per-workgroup phase cycles
 };
 
@@ -242,17 +226,13 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if ((uint32_t)(uintptr_t)(lds_u32*)lds != 0u) __builtin_trap();   // raw LDS addresses assume base 0
-    for (uint32_t i = tid; i < L::lds_bytes / 4; i += kBkBlock) lds[i] = 0;   // histogram, counters, barriers
+    for (uint32_t i = tid; i < kBkCodes + NBK; i += kBkBlock) lds[i] = 0;   // histogram + counters
     __syncthreads();
 
     uint16_t* rec = B.rec + (uint64_t)blockIdx.x * L::rec_cap;
-    uint16_t* meta = B.meta + (uint64_t)blockIdx.x * (NBK + 1) * kRuns;
-    uint32_t* roff = B.roff + (uint64_t)blockIdx.x * kRuns;
+    uint16_t* meta = B.meta + (uint64_t)blockIdx.x * (NBK + 1) * kRmax;
+    uint32_t* roff = B.roff + (uint64_t)blockIdx.x * kRmax;
     const uint32_t npiece = B.pstart[A.n_genomes];
-    // phase-1 half of this wave, its wave and thread index within the half
-    const uint32_t hf = (uint32_t)wave / kHalfWaves, wh = (uint32_t)wave % kHalfWaves;
-    const uint32_t tid_h = (uint32_t)tid % kHalfBlock;
-    uint32_t nsync = 0;   // arrivals at this half's barrier so far (the counter is never reset)
 
     for (uint32_t p = blockIdx.x; p < npiece; p += gridDim.x) {
         // genome of piece p: last g with pstart[g] <= p
@@ -262,13 +242,12 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
         const uint64_t plo = split_at(glo, ghi, pi, np), phi = split_at(glo, ghi, pi + 1, np);
         const uint64_t lo = split_at(plo, phi, wave, kBkWaves), hi = split_at(plo, phi, wave + 1, kBkWaves);
-        // rounds of each half = its longest wave range in chunks (same in every wave)
-        uint32_t nr[kBkHalves] = {0u, 0u};
+        // rounds = the longest wave range in chunks (same value in every wave)
+        uint32_t nround = 0;
         for (int w = 0; w < kBkWaves; ++w) {
             const uint64_t a = split_at(plo, phi, w, kBkWaves), e = split_at(plo, phi, w + 1, kBkWaves);
-            if (e > a) nr[w / kHalfWaves] = max(nr[w / kHalfWaves], (uint32_t)((e - (a & ~(uint64_t)15) + kChunk - 1) / kChunk));
+            if (e > a) nround = max(nround, (uint32_t)((e - (a & ~(uint64_t)15) + kChunk - 1) / kChunk));
         }
-        const uint32_t nround = hf ? nr[1] : nr[0];
 
         // ---------------------------------------------------------- phase 1
         const uint64_t t_p1 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -285,46 +264,29 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         if (lo < hi) rg.warm<K>(A, lane);
         uint32_t carry = lo < hi ? rg.carry : 0u;
         uint32_t rel = 0;
-        // Per half, one barrier per round.  Round r: zero the counter set of
-        // round r+1, count + rank this round's records in set r % 3, barrier;
-        // then copy out round r-1 (staged in the other buffer before this
-        // barrier), every wave computes the bucket offsets of round r into its
-        // private table (no serial scan, no second barrier), and stages its
-        // records.  A counter set is zeroed two rounds after its last read, so
-        // the barriers order it.
-        for (uint32_t i = tid; i < 3 * kBkHalves * NBK; i += kBkBlock) lds_st(L::cnt + 4 * i, 0u);
+        // One barrier per round.  Round r: zero the counter set of round r+1,
+        // count + rank this round's records in set r % 3, barrier; then copy out
+        // round r-1 (staged in the other buffer before this barrier), every wave
+        // computes the bucket offsets of round r into its private table (no
+        // serial scan, no second barrier), and stages its records.  A counter set
+        // is zeroed two rounds after its last read, so the barriers order it.
+        for (uint32_t i = tid; i < 3 * NBK; i += kBkBlock) lds_st(L::cnt + 4 * i, 0u);
         lds_barrier();
-        const uint32_t bar = L::bar + 4 * hf;
-        // barrier of this half's 8 waves: every LDS operation of a wave is done
-        // before its arrival (lgkmcnt(0)), arrivals are counted in LDS, and a wave
-        // leaves once the count reaches its target (the counter only grows)
-        auto half_sync = [&]() {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            nsync += kHalfWaves;
-            if (lane == 0) lds_add(bar, 1u);
-            for (uint32_t spin = 0;; ++spin) {
-                const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(
-                    (int)__hip_atomic_load((lds_u32*)(uintptr_t)bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if (v >= nsync) break;
-                if (spin >= (1u << 24)) __builtin_trap();   // a lost arrival: fail loudly, never hang
-                __builtin_amdgcn_s_sleep(1);
-            }
-            asm volatile("" ::: "memory");
-        };
-        uint32_t off = (uint32_t)(hf * L::rec_cap_half);   // records of this half's rounds before the current one
+        uint64_t p1w = 0;                    // profile: phase-1 barrier wait of this wave
+        uint32_t off = 0;                    // records of rounds before the current one (x8)
         uint32_t t_prev = 0, off_prev = 0;   // last staged round, copied out one round later
-        const uint32_t rb = L::rbase(hf) + wh * (NBK + 1) * 4;
+        const uint32_t rb = L::rbase + (uint32_t)wave * (NBK + 1) * 4;
         auto copy_out = [&](uint32_t r, uint32_t T, uint32_t o) {
-            const uint32_t st = L::stage(hf, r);
-            for (uint32_t q = tid_h; q < T / 8; q += kHalfBlock) {
+            const uint32_t st = L::stage + (r & 1) * L::stage_bytes;
+            for (uint32_t q = tid; q < T / 8; q += kBkBlock) {
                 const v4u v = *(lds_v4u*)(uintptr_t)(st + 16 * q);
                 *(v4u*)(rec + o + 8 * q) = v;
             }
         };
         auto round = [&](uint32_t r, uint4& bf) {
-            const uint32_t cb = L::cnt + 4 * NBK * (3 * hf + r % 3);
-            const uint32_t cz = L::cnt + 4 * NBK * (3 * hf + (r + 1) % 3);
-            for (uint32_t b = tid_h; b < NBK; b += kHalfBlock) lds_st(cz + 4 * b, 0u);
+            const uint32_t cb = L::cnt + 4 * NBK * (r % 3);
+            const uint32_t cz = L::cnt + 4 * NBK * ((r + 1) % 3);
+            for (uint32_t b = tid; b < NBK; b += kBkBlock) lds_st(cz + 4 * b, 0u);
             uint32_t s[16], rk[16];
             const bool have = r < nch;
             bool dense = false;   // wave-uniform: windows 0..14 of every lane are valid (fast case)
@@ -341,6 +303,11 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
 #pragma unroll
 #if KF_BK_ABL == 3   // profiling only: no rank atomics (ranks by lane: wrong counts)
                     for (int j = 0; j < 15; ++j) rk[j] = (uint32_t)lane * 16 + j;
+#elif KF_BK_ABL == 7   // profiling only: rank adds without returns (ranks by lane: wrong counts)
+                    for (int j = 0; j < 15; ++j) {
+                        lds_add(cb + ((s[j] >> kBkBits) << 2), 1u);
+                        rk[j] = (uint32_t)lane * 16 + j;
+                    }
 #else
                     for (int j = 0; j < 15; ++j) rk[j] = lds_add_rtn(cb + ((s[j] >> kBkBits) << 2), 1u);
 #endif
@@ -363,7 +330,14 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                 rel += kChunk;
                 if (rel + 3 * kChunk < nch * kChunk) bf = rg.load(A.bytes, rel + 3 * kChunk, lane);
             }
-            half_sync();
+            if (B.prof) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const uint64_t t = __builtin_amdgcn_s_memtime();
+                lds_barrier();
+                p1w += __builtin_amdgcn_s_memtime() - t;
+            } else {
+                lds_barrier();
+            }
             if (r > 0) copy_out(r - 1, t_prev, off_prev);
             // bucket offsets of round r (exclusive prefix over buckets), per wave
             constexpr uint32_t PER = (NBK + kWave - 1) / kWave;
@@ -380,23 +354,22 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             const uint32_t inc = wave_incl_scan(sum);
             const uint32_t ex = inc - sum;
             const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-            const uint32_t run = hf * kRmax + r;
 #pragma unroll
             for (uint32_t j = 0; j < PER; ++j) {
                 const uint32_t b = (uint32_t)lane * PER + j;
                 if (b < NBK) {
                     lds_st(rb + 4 * b, ex + loc[j]);
-                    if (wh == 0) meta[(uint64_t)b * kRuns + run] = (uint16_t)(ex + loc[j]);
+                    if (wave == 0) meta[(uint64_t)b * kRmax + r] = (uint16_t)(ex + loc[j]);
                 }
             }
-            if (wh == 0 && lane == kWave - 1) {
-                meta[(uint64_t)NBK * kRuns + run] = (uint16_t)T;
-                roff[run] = off;
+            if (wave == 0 && lane == kWave - 1) {
+                meta[(uint64_t)NBK * kRmax + r] = (uint16_t)T;
+                roff[r] = off;
             }
-            const uint32_t st = L::stage(hf, r);
-            // sentinels after each run, up to its unit boundary (one wave of the
-            // half per round, rotating)
-            if ((r % kHalfWaves) == wh) {
+            const uint32_t st = L::stage + (r & 1) * L::stage_bytes;
+            // sentinels after each run, up to its unit boundary (one wave per
+            // round, rotating)
+            if ((r % kBkWaves) == (uint32_t)wave) {
 #pragma unroll
                 for (uint32_t j = 0; j < PER; ++j) {
                     const uint32_t b = (uint32_t)lane * PER + j;
@@ -444,9 +417,8 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         if (r < nround) round(r++, buf[0]);
         if (r < nround) round(r++, buf[1]);
         if (r < nround) round(r++, buf[2]);
-        half_sync();
+        lds_barrier();
         if (nround > 0) copy_out(nround - 1, t_prev, off_prev);
-        const uint64_t p1w = 0;
 
         // ---------------------------------------------------------- phase 2
         // records and meta were stored by other waves of this workgroup: wait for
@@ -458,27 +430,35 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         uint32_t* row = A.counts + (uint64_t)g * A.nbins;
         const bool split = np > 1;
         unsigned long long tsum = 0;
-        // Run table of this wave: lane j (< nrun) <-> run wave + 16 j of the
-        // bucket's runs (half 0's rounds, then half 1's).  A run is the whole
-        // units of one bucket in one half-round (padded by phase 1), and the units
-        // of all the wave's runs are laid end to end (prefix P over lanes), so
-        // every load instruction carries 64 units whatever the run lengths.  The
-        // next bucket's first group is issued before this bucket's flush, so its
-        // loads are in flight during the flush.  Loads are unconditional
-        // (inactive lanes read unit 0) so vmcnt stays exact.
-        const uint32_t myr = (uint32_t)wave + kBkWaves * (uint32_t)lane;
-        const uint32_t nrt = nr[0] + nr[1];
-        const bool myr_ok = myr < nrt;
-        const uint32_t myrun = myr < nr[0] ? myr : kRmax + (myr - nr[0]);
-
-        const uint32_t myr_c = myr_ok ? myrun : 0u;
+        // Run table of this wave: lane j (< nrun) <-> round wave + 16 j.  A run is
+        // the whole units of one bucket in one round (padded by phase 1), and the
+        // units of all the wave's runs are laid end to end (prefix P over lanes),
+        // so every load instruction carries 64 units whatever the run lengths.
+        // A group is kGW windows of 64 units (512 units: a whole k=11 bucket of a
+        // wave, typically); the next bucket's first group is issued before this
+        // bucket's flush, so its loads are in flight during the flush.  Loads are
+        // unconditional (inactive lanes read unit 0) so vmcnt stays exact.
+        // Rounds are dealt to waves in patterns of 4 (a0 + a1 + a2 + a3) rounds, a_s
+        // consecutive rounds to each wave of slot s = wave >> 2 (its age on its
+        // SIMD: older slots issue first and finish sooner, so they may take more);
+        // a = 1,1,1,1 is round wave + 16 j.  The valid runs are lanes 0 .. nrun-1.
+        const uint32_t slot = (uint32_t)wave >> 2;
+        const uint32_t a_s = (B.slot_w >> (8 * slot)) & 0xFFu;
+        const uint32_t a_below = ((B.slot_w & 0xFFu) * (slot > 0)) + (((B.slot_w >> 8) & 0xFFu) * (slot > 1)) +
+                                 (((B.slot_w >> 16) & 0xFFu) * (slot > 2));
+        const uint32_t per = 4 * ((B.slot_w & 0xFFu) + ((B.slot_w >> 8) & 0xFFu) + ((B.slot_w >> 16) & 0xFFu) +
+                                  (B.slot_w >> 24));
+        const uint32_t lq = (uint32_t)lane / a_s;
+        const uint32_t myr = lq * per + 4 * a_below + ((uint32_t)wave & 3u) * a_s + ((uint32_t)lane - lq * a_s);
+        const bool myr_ok = myr < nround;
+        const uint32_t myr_c = myr_ok ? myr : 0u;
         const uint32_t nrun = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(myr_ok));
         const uint32_t ro_l = __builtin_nontemporal_load(roff + myr_c);
         const uint32_t ro = myr_ok ? ro_l : 0u;
         // raw (lanes without a run read round 0; make_tbl masks them), so that
         // the load is not waited for until its table is built
         auto meta_at = [&](uint32_t b) -> uint32_t {
-            return __builtin_nontemporal_load(meta + (uint64_t)b * kRuns + myr_c);
+            return __builtin_nontemporal_load(meta + (uint64_t)b * kRmax + myr_c);
         };
         struct Tbl {
             uint32_t P, DL;          // per lane (run): first unit in the bucket's unit space, unit delta
@@ -713,6 +693,28 @@ uint32_t bucket_lds_for(int k) {
     }
 }
 
+// Phase-2 rounds per wave by wave slot, packed 4 x 8 bit (slot 0 in the low byte).
+// KF_BK_WEIGHTS="a0,a1,a2,a3" (tuning/A-B knob, read per launch), each 1..32; a set
+// that could give a wave more than 64 runs of a piece is refused (default used).
+uint32_t bucket_weights() {
+    constexpr uint32_t kDefault = 0x01010101u;
+#ifndef KF_PROFILE_BUILD
+    return kDefault;   // the knob is read in profiling builds only
+#endif
+    const char* e = getenv("KF_BK_WEIGHTS");
+    if (!e || !*e) return kDefault;
+    unsigned a[4];
+    if (sscanf(e, "%u,%u,%u,%u", &a[0], &a[1], &a[2], &a[3]) != 4) return kDefault;
+    uint32_t per = 0, amax = 0;
+    for (int i = 0; i < 4; ++i) {
+        if (a[i] < 1 || a[i] > 32) return kDefault;
+        per += 4 * a[i];
+        amax = a[i] > amax ? a[i] : amax;
+    }
+    if ((kRmax / per + 1) * amax > (uint32_t)kWave) return kDefault;
+    return a[0] | a[1] << 8 | a[2] << 16 | a[3] << 24;
+}
+
 // Per-device state: bucket tables per k and the scratch of the last launch
 // size.  A launch on another stream waits for the previous user of the scratch.
 struct DevState {
@@ -799,9 +801,9 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     const int grid = d.grid;
     // scratch: records, round metadata (sized for the largest k), round offsets
     const size_t nbk = ((size_t)1 << (2 * k)) >> kBkBits;
-    const size_t rec_b = (size_t)grid * kBkHalves * ((size_t)kRmax * (kRoundRecs + 7 * nbk) + 8) * 2;   // Bk<k>::rec_cap
-    const size_t meta_b = (size_t)grid * (((1u << (2 * KF_MAX_K)) >> kBkBits) + 1) * kRuns * 2;
-    const size_t roff_b = (size_t)grid * kRuns * 4;
+    const size_t rec_b = (size_t)grid * ((size_t)kRmax * (kRoundRecs + 7 * nbk) + 8) * 2;   // Bk<k>::rec_cap
+    const size_t meta_b = (size_t)grid * (((1u << (2 * KF_MAX_K)) >> kBkBits) + 1) * kRmax * 2;
+    const size_t roff_b = (size_t)grid * kRmax * 4;
     const size_t need = rec_b + meta_b + roff_b;
     if (d.done && hipStreamWaitEvent(s, d.done, 0) != hipSuccess)
         return kf_fail(KF_EHIP, "hipStreamWaitEvent failed");
@@ -831,6 +833,7 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     B.meta = (uint16_t*)((char*)d.scratch + rec_b);
     B.roff = (uint32_t*)((char*)d.scratch + rec_b + meta_b);
     B.accumulate = (flags & KF_ACCUMULATE) ? 1u : 0u;
+    B.slot_w = bucket_weights();
     B.prof = nullptr;
 #ifdef KF_PROFILE_BUILD
     const char* pe = getenv("KF_BUCKET_PROFILE");   // debugging aid: synchronous, prints to stderr
