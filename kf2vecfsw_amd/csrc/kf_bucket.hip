@@ -61,25 +61,59 @@ constexpr uint32_t kRmax = (uint32_t)(kPieceMax / kRoundRecs) + 2;
 // area past the histogram, so a 16-byte unit never needs a range test.
 constexpr uint32_t kSentinel = 0x8000u;
 
+// Phase-1 rank counters: each bucket's round counter is split into R = 2^rl
+// lane replicas (lane L ranks into replica L mod R), so the 64 lanes of one
+// ds_add_rtn spread over the banks instead of piling onto the few counters of
+// random buckets.  A round's table has nbk x R entries (bucket major), 1 to 8
+// per lane.  Measured (tools/lds_rank_rate.hip, cycles per wave-instruction per
+// CU): 8 shared counters 28.7 -> 7.3 with 64 replicas; 32: 13.7 -> 7.3; 128:
+// 11.2 -> 8.7 with 4.  In the kernel (profiles/r03/v5_lib_ab_k*_rank_replicas.json,
+// one process): k = 9 R = 32 6.39 ms (shared counters 9.05), k = 10 R = 16 7.27
+// (7.51); k = 11 stays at R = 1 (R = 4: 9.59 vs 9.24, its 512-entry tables cost
+// more than the conflicts they remove).  log2 R per k (KF_BK_RL<k>, tools/ only):
+#ifndef KF_BK_RL9
+#define KF_BK_RL9 5
+#endif
+#ifndef KF_BK_RL10
+#define KF_BK_RL10 4
+#endif
+#ifndef KF_BK_RL11
+#define KF_BK_RL11 0
+#endif
+#ifndef KF_BK_RL12
+#define KF_BK_RL12 0
+#endif
+constexpr uint32_t bk_rl(int K) {
+    return K == 9 ? KF_BK_RL9 : K == 10 ? KF_BK_RL10 : K == 11 ? KF_BK_RL11 : KF_BK_RL12;
+}
+
 template <int K>
 struct Bk {
     static constexpr uint32_t nbk = (1u << (2 * K)) >> kBkBits;   // buckets
+    static constexpr uint32_t rl = bk_rl(K);
+    static constexpr uint32_t nrep = 1u << rl;                      // rank replicas per bucket
+    static constexpr uint32_t nent = nbk << rl;                     // rank entries per round
+    static constexpr uint32_t epl = nent / kWave;                   // rank entries per lane
     static constexpr uint32_t round_cap = kRoundRecs + 7 * nbk;     // records of a padded round
     static constexpr uint64_t rec_cap = (uint64_t)kRmax * round_cap + 8;   // per workgroup
     // LDS byte layout.  Phase 2: the 128 KiB histogram at 0.  Phase 1 reuses it:
-    // two round staging buffers, then one private bucket-offset table per wave.
-    // After the histogram: three rotating sets of round rank counters (phase 1),
-    // which phase 2 reuses as the sentinels' trash bins, and the reduction slots.
+    // two round staging buffers, then one private rank-entry offset table per
+    // wave.  After the histogram: three rotating sets of round rank counters
+    // (phase 1), which phase 2 reuses as the sentinels' trash bins, and the
+    // reduction slots.
     static constexpr uint32_t hist = 0;
     static constexpr uint32_t stage_bytes = (round_cap * 2 + 15) & ~15u;
     static constexpr uint32_t stage = 0;                            // + (r & 1) * stage_bytes
-    static constexpr uint32_t rbase = 2 * stage_bytes;              // + wave * (nbk + 1) * 4
-    static constexpr uint32_t dirty = rbase + kBkWaves * (nbk + 1) * 4;   // phase-1 footprint in hist
-    static constexpr uint32_t cnt = kBkCodes * 4;                   // + (r % 3) * nbk * 4
-    static constexpr uint32_t red = (cnt + 3 * nbk * 4 + 7) & ~7u;  // kBkWaves u64
+    static constexpr uint32_t tbl_bytes = nent * 4 + 16;            // per wave (16-byte aligned)
+    static constexpr uint32_t rbase = 2 * stage_bytes;              // + wave * tbl_bytes
+    static constexpr uint32_t dirty = rbase + kBkWaves * tbl_bytes;   // phase-1 footprint in hist
+    static constexpr uint32_t cnt = kBkCodes * 4;                   // + (r % 3) * nent * 4
+    static constexpr uint32_t red = (cnt + 3 * nent * 4 + 7) & ~7u; // kBkWaves u64
     static constexpr uint32_t lds_bytes =
         red + kBkWaves * 8 > cnt + 256 ? red + kBkWaves * 8 : cnt + 256;   // trash: 64 bins at cnt
+    static_assert(epl >= 1 && epl <= 8 && (epl & (epl - 1)) == 0 && nent == epl * kWave, "1-8 entries per lane");
     static_assert(dirty <= kBkCodes * 4, "phase-1 tables must fit the histogram area");
+    static_assert(lds_bytes <= 160 * 1024, "LDS");
     static_assert(round_cap < 65536, "round offsets are u16");
 };
 
@@ -118,6 +152,36 @@ __device__ __forceinline__ uint32_t rec_addr(uint32_t d, int h) {
 }
 __device__ __forceinline__ uint32_t lds_ld(uint32_t a) { return *(volatile lds_u32*)(uintptr_t)a; }
 __device__ __forceinline__ void lds_st(uint32_t a, uint32_t v) { *(volatile lds_u32*)(uintptr_t)a = v; }
+typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) v2u_t lds_v2u;
+// N consecutive words at a (N = 1, 2, 4, 8; a aligned to min(4 N, 16) bytes)
+template <uint32_t N>
+__device__ __forceinline__ void lds_ldn(uint32_t a, uint32_t (&v)[N]) {
+    if constexpr (N == 1) {
+        v[0] = lds_ld(a);
+    } else if constexpr (N == 2) {
+        const v2u_t x = *(volatile lds_v2u*)(uintptr_t)a;
+        v[0] = x.x, v[1] = x.y;
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < N / 4; ++i) {
+            const v4u x = *(volatile lds_v4u*)(uintptr_t)(a + 16 * i);
+            v[4 * i] = x.x, v[4 * i + 1] = x.y, v[4 * i + 2] = x.z, v[4 * i + 3] = x.w;
+        }
+    }
+}
+template <uint32_t N>
+__device__ __forceinline__ void lds_stn(uint32_t a, const uint32_t (&v)[N]) {
+    if constexpr (N == 1) {
+        lds_st(a, v[0]);
+    } else if constexpr (N == 2) {
+        *(volatile lds_v2u*)(uintptr_t)a = v2u_t{v[0], v[1]};
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < N / 4; ++i)
+            *(volatile lds_v4u*)(uintptr_t)(a + 16 * i) = v4u{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+    }
+}
 // Barrier for LDS traffic only: outstanding global loads (the byte-stream
 // prefetch) stay in flight across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -270,12 +334,15 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         // computes the bucket offsets of round r into its private table (no
         // serial scan, no second barrier), and stages its records.  A counter set
         // is zeroed two rounds after its last read, so the barriers order it.
-        for (uint32_t i = tid; i < 3 * NBK; i += kBkBlock) lds_st(L::cnt + 4 * i, 0u);
+        for (uint32_t i = tid; i < 3 * L::nent; i += kBkBlock) lds_st(L::cnt + 4 * i, 0u);
         lds_barrier();
         uint64_t p1w = 0;                    // profile: phase-1 barrier wait of this wave
         uint32_t off = 0;                    // records of rounds before the current one (x8)
         uint32_t t_prev = 0, off_prev = 0;   // last staged round, copied out one round later
-        const uint32_t rb = L::rbase + (uint32_t)wave * (NBK + 1) * 4;
+        const uint32_t rb = L::rbase + (uint32_t)wave * L::tbl_bytes;
+        // byte offset of the rank entry of canonical code s for this lane (its replica)
+        const uint32_t repo = ((uint32_t)lane & (L::nrep - 1u)) << 2;
+        auto ent = [&](uint32_t s) -> uint32_t { return ((s >> kBkBits) << (L::rl + 2)) | repo; };
         auto copy_out = [&](uint32_t r, uint32_t T, uint32_t o) {
             const uint32_t st = L::stage + (r & 1) * L::stage_bytes;
             for (uint32_t q = tid; q < T / 8; q += kBkBlock) {
@@ -284,9 +351,9 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             }
         };
         auto round = [&](uint32_t r, uint4& bf) {
-            const uint32_t cb = L::cnt + 4 * NBK * (r % 3);
-            const uint32_t cz = L::cnt + 4 * NBK * ((r + 1) % 3);
-            for (uint32_t b = tid; b < NBK; b += kBkBlock) lds_st(cz + 4 * b, 0u);
+            const uint32_t cb = L::cnt + 4 * L::nent * (r % 3);
+            const uint32_t cz = L::cnt + 4 * L::nent * ((r + 1) % 3);
+            for (uint32_t e = tid; e < L::nent; e += kBkBlock) lds_st(cz + 4 * e, 0u);
             uint32_t s[16], rk[16];
             const bool have = r < nch;
             bool dense = false;   // wave-uniform: windows 0..14 of every lane are valid (fast case)
@@ -305,13 +372,13 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                     for (int j = 0; j < 15; ++j) rk[j] = (uint32_t)lane * 16 + j;
 #elif KF_BK_ABL == 7   // profiling only: rank adds without returns (ranks by lane: wrong counts)
                     for (int j = 0; j < 15; ++j) {
-                        lds_add(cb + ((s[j] >> kBkBits) << 2), 1u);
+                        lds_add(cb + ent(s[j]), 1u);
                         rk[j] = (uint32_t)lane * 16 + j;
                     }
 #else
-                    for (int j = 0; j < 15; ++j) rk[j] = lds_add_rtn(cb + ((s[j] >> kBkBits) << 2), 1u);
+                    for (int j = 0; j < 15; ++j) rk[j] = lds_add_rtn(cb + ent(s[j]), 1u);
 #endif
-                    if (s[15] != 0xFFFFFFFFu) rk[15] = lds_add_rtn(cb + ((s[15] >> kBkBits) << 2), 1u);
+                    if (s[15] != 0xFFFFFFFFu) rk[15] = lds_add_rtn(cb + ent(s[15]), 1u);
                 } else {
                     uint32_t C, V, EN, ne, own;
                     if (msk) {
@@ -325,7 +392,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                     canon_std<K>(w, s);
 #pragma unroll
                     for (int j = 0; j < 16; ++j)
-                        if (s[j] != 0xFFFFFFFFu) rk[j] = lds_add_rtn(cb + ((s[j] >> kBkBits) << 2), 1u);
+                        if (s[j] != 0xFFFFFFFFu) rk[j] = lds_add_rtn(cb + ent(s[j]), 1u);
                 }
                 rel += kChunk;
                 if (rel + 3 * kChunk < nch * kChunk) bf = rg.load(A.bytes, rel + 3 * kChunk, lane);
@@ -339,28 +406,77 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                 lds_barrier();
             }
             if (r > 0) copy_out(r - 1, t_prev, off_prev);
-            // bucket offsets of round r (exclusive prefix over buckets), per wave
-            constexpr uint32_t PER = (NBK + kWave - 1) / kWave;
-            uint32_t loc[PER], cntv[PER];
-            uint32_t sum = 0;
+            // rank-entry offsets of round r, per wave (no serial scan, no second
+            // barrier): entry e = b R + replica, bucket major, lane L holds entries
+            // EPL L .. EPL L + EPL - 1.  A bucket's run is its replicas' records end
+            // to end, padded to whole 8-record units.
+            constexpr uint32_t NR = L::nrep, EPL = L::epl;
+            constexpr uint32_t BPL = NR >= EPL ? 1u : EPL / NR;   // buckets described by this lane
+            uint32_t c[EPL];
+            lds_ldn<EPL>(cb + 4 * EPL * lane, c);
+            uint32_t o[EPL];               // offsets of the lane's entries
+            uint32_t T;                    // padded records of the round
+            uint32_t bst[BPL], bcnt[BPL];  // run start and record count of the lane's buckets
+            bool bown = true;              // this lane describes them (meta, sentinels)
+            if constexpr (NR >= EPL) {
+                // a bucket spans G lanes: segmented scan, then the padded runs
+                // ended by each bucket's last lane
+                constexpr int G = (int)(NR / EPL);
+                uint32_t lp = 0;
 #pragma unroll
-            for (uint32_t j = 0; j < PER; ++j) {
-                const uint32_t b = (uint32_t)lane * PER + j;
-                const uint32_t v = b < NBK ? lds_ld(cb + 4 * b) : 0u;
-                loc[j] = sum;
-                cntv[j] = v;
-                sum += (v + 7) & ~7u;   // runs padded to whole units
-            }
-            const uint32_t inc = wave_incl_scan(sum);
-            const uint32_t ex = inc - sum;
-            const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-#pragma unroll
-            for (uint32_t j = 0; j < PER; ++j) {
-                const uint32_t b = (uint32_t)lane * PER + j;
-                if (b < NBK) {
-                    lds_st(rb + 4 * b, ex + loc[j]);
-                    if (wave == 0) meta[(uint64_t)b * kRmax + r] = (uint16_t)(ex + loc[j]);
+                for (int j = 0; j < (int)EPL; ++j) {
+                    o[j] = lp;
+                    lp += c[j];
                 }
+                const uint32_t inc = wave_incl_scan(lp), exc = inc - lp;
+                const int first = lane & ~(G - 1), last = first + G - 1;
+                const uint32_t seg0 = (uint32_t)__shfl((int)exc, first, kWave);
+                const uint32_t tot = (uint32_t)__shfl((int)inc, last, kWave) - seg0;
+                const uint32_t pad = lane == last ? (tot + 7u) & ~7u : 0u;
+                const uint32_t binc = wave_incl_scan(pad);
+                const uint32_t base = binc - pad;   // padded runs of the buckets before
+                const uint32_t add = base + (exc - seg0);
+#pragma unroll
+                for (int j = 0; j < (int)EPL; ++j) o[j] += add;
+                T = (uint32_t)__builtin_amdgcn_readlane((int)binc, kWave - 1);
+                bst[0] = base;
+                bcnt[0] = tot;
+                bown = lane == first;
+            } else {
+                // BPL whole buckets of NR entries per lane
+                uint32_t tot[BPL], lsum = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < BPL; ++q) {
+                    tot[q] = 0;
+#pragma unroll
+                    for (uint32_t t = 0; t < NR; ++t) tot[q] += c[q * NR + t];
+                    lsum += (tot[q] + 7u) & ~7u;
+                }
+                const uint32_t inc = wave_incl_scan(lsum);
+                uint32_t base = inc - lsum;
+                T = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+#pragma unroll
+                for (uint32_t q = 0; q < BPL; ++q) {
+                    bst[q] = base;
+                    bcnt[q] = tot[q];
+                    uint32_t x = base;
+#pragma unroll
+                    for (uint32_t t = 0; t < NR; ++t) {
+                        o[q * NR + t] = x;
+                        x += c[q * NR + t];
+                    }
+                    base += (tot[q] + 7u) & ~7u;
+                }
+            }
+            lds_stn<EPL>(rb + 4 * EPL * lane, o);
+            // bucket of the lane's q-th described run
+            auto bid = [&](uint32_t q) -> uint32_t {
+                if constexpr (NR >= EPL) return (uint32_t)lane / (NR / EPL);
+                else return (uint32_t)lane * BPL + q;
+            };
+            if (wave == 0 && bown) {
+#pragma unroll
+                for (uint32_t q = 0; q < BPL; ++q) meta[(uint64_t)bid(q) * kRmax + r] = (uint16_t)bst[q];
             }
             if (wave == 0 && lane == kWave - 1) {
                 meta[(uint64_t)NBK * kRmax + r] = (uint16_t)T;
@@ -369,21 +485,20 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             const uint32_t st = L::stage + (r & 1) * L::stage_bytes;
             // sentinels after each run, up to its unit boundary (one wave per
             // round, rotating)
-            if ((r % kBkWaves) == (uint32_t)wave) {
+            if ((r % kBkWaves) == (uint32_t)wave && bown) {
 #pragma unroll
-                for (uint32_t j = 0; j < PER; ++j) {
-                    const uint32_t b = (uint32_t)lane * PER + j;
-                    const uint32_t e = ex + loc[j] + cntv[j], npad = (8u - (cntv[j] & 7u)) & 7u;
+                for (uint32_t q = 0; q < BPL; ++q) {
+                    const uint32_t e = bst[q] + bcnt[q], npad = (8u - (bcnt[q] & 7u)) & 7u;
 #pragma unroll
                     for (uint32_t x = 0; x < 7; ++x)
-                        if (b < NBK && x < npad)
+                        if (x < npad)
                             *(volatile lds_u16*)(uintptr_t)(st + 2 * (e + x)) = (uint16_t)(kSentinel | ((e + x) & 63u));
                 }
             }
             if (dense) {
 #pragma unroll
                 for (int j = 0; j < 15; ++j) {
-                    const uint32_t slot = lds_ld(rb + ((s[j] >> kBkBits) << 2)) + rk[j];
+                    const uint32_t slot = lds_ld(rb + ent(s[j])) + rk[j];
 #if KF_BK_ABL == 4   // profiling only: no staging writes (wrong counts)
                     asm volatile("" ::"v"(slot), "v"(s[j]));
 #else
@@ -391,14 +506,14 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
 #endif
                 }
                 if (s[15] != 0xFFFFFFFFu) {
-                    const uint32_t slot = lds_ld(rb + ((s[15] >> kBkBits) << 2)) + rk[15];
+                    const uint32_t slot = lds_ld(rb + ent(s[15])) + rk[15];
                     *(volatile lds_u16*)(uintptr_t)(st + 2 * slot) = (uint16_t)(s[15] & (kBkCodes - 1));
                 }
             } else if (have) {
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     if (s[j] != 0xFFFFFFFFu) {
-                        const uint32_t slot = lds_ld(rb + ((s[j] >> kBkBits) << 2)) + rk[j];
+                        const uint32_t slot = lds_ld(rb + ent(s[j])) + rk[j];
                         *(volatile lds_u16*)(uintptr_t)(st + 2 * slot) = (uint16_t)(s[j] & (kBkCodes - 1));
                     }
                 }
