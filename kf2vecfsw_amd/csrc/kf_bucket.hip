@@ -37,7 +37,7 @@ namespace kf {
 // wrong): 1 = no col_idx table reads in the flush, 2 = no record reads in phase
 // 2 (hashed stand-ins), 3 = no phase-1 rank atomics (dense path), 4 = no
 // phase-1 staging writes (dense path), 5 = no phase-2 histogram adds, 7 = rank
-// adds without returns.
+// adds without returns, 8 = no phase 2 (rows stay zero).
 #ifndef KF_BK_ABL
 #define KF_BK_ABL 0
 #endif
@@ -706,7 +706,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         issue(tb, G0);
         uint64_t tp[4] = {0, 0, 0, 0};   // profile: records, barrier, flush, barrier
         uint64_t tcons = 0;              // profile: consume part of records
-        for (uint32_t b = 0; b < NBK; ++b) {
+        for (uint32_t b = 0; b < (KF_BK_ABL == 8 ? 0u : NBK); ++b) {   // (ABL 8: phase 1 only)
             uint64_t t0 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
 #if KF_BK_DB
             // two groups alternate: the bucket's next group is always in flight
