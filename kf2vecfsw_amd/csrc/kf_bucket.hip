@@ -35,7 +35,8 @@ namespace kf {
 
 // Profiling-only ablations (-DKF_BK_ABL=n through KF_HIPCC_FLAGS; counts are
 // wrong): 1 = no col_idx table reads in the flush, 2 = no record reads in phase
-// 2 (hashed stand-ins), 3 = no phase-1 rank atomics (dense path), 4 = no
+// 2 (hashed stand-ins), 3 = no phase-1 rank atomics (dense path; the round counts
+// stay 0, so no records are written or read at all), 4 = no
 // phase-1 staging writes (dense path), 5 = no phase-2 histogram adds, 7 = rank
 // adds without returns, 8 = no phase 2 (rows stay zero).
 #ifndef KF_BK_ABL
