@@ -503,6 +503,180 @@ __device__ __forceinline__ uint32_t x_body8(const XCls& k, uint32_t& carry, uint
     return o;
 }
 
+// ---------------------------------------------------------------- K1x, coalesced layout
+// KF_XC = 1: the 3 KiB iteration is read as three 1 KiB regions, lane L holding
+// bytes [16L, 16L+16) of each, so every load instruction reads 1 KiB contiguous,
+// with the non-temporal cache policy.  Measured streaming rate of the two layouts
+// (tools/cpol_rate.hip, profiles/r03/v8_cpol_rate.txt): 6.8 TB/s coalesced + nt vs
+// 5.6-5.8 TB/s for 48-byte lanes, which the nt bit slows to 4.5.  Windows are
+// formed and paired per 16-byte region: a lane holds 16 entries (15 with a
+// newline), the k-1 entries of context come from lane L-1's region by DPP, lane
+// 0 takes the previous region's lane 63.
+#ifndef KF_XC
+#define KF_XC 1
+#endif
+constexpr int kXNt = 2;   // buffer-load cache policy bit: non-temporal
+
+__device__ __forceinline__ XBlock xc_load(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r, int lane) {
+    // clamped to the genome end rounded up to 16 B (load_chunk): bytes past it read 0
+    const uint32_t rec = end_r > rel ? min(end_r - rel, (uint32_t)kXChunk) : 0u;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c0 + rel), (short)0, (int)rec, 0x00020000);
+    XBlock b;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + kChunk * i, 0, kXNt);
+        b.q[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    return b;
+}
+
+// dot4 weights of dword i of a 16-byte region in its newline test: byte b = 4i + t
+// weighs 2 (32 - b), so V = 0 without a newline, 34 + 2e for one newline at entry
+// e = 15 - b (<= 64), and >= 68 otherwise (every further nonzero z adds >= 34, a
+// bad byte's z >= 2)
+__device__ __forceinline__ constexpr uint32_t xc_nl_weights(int i) {
+    return (uint32_t)(64 - 8 * i) | (uint32_t)(62 - 8 * i) << 8 | (uint32_t)(60 - 8 * i) << 16 |
+           (uint32_t)(58 - 8 * i) << 24;
+}
+constexpr uint32_t kXcBad = 68u;   // V at or above: not the fast case
+
+// One region's codes (entry 0 = byte 15) and newline / bad-byte sum (as x_cls).
+struct XcCls {
+    uint32_t C, V;
+};
+__device__ __forceinline__ XcCls xc_cls(const uint4 d) {
+    const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+    const uint32_t cdf = 0xDFDFDFDFu;
+    uint32_t pc[4], z[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t x = w[i];
+        const uint32_t e = __builtin_amdgcn_perm(kXTabHi, kXTabLo, x & 0x07070707u);
+        z[i] = x_zmap(x, e, cdf);
+        pc[i] = __builtin_amdgcn_udot4(x & 0x06060606u, 0x01041040u, (i & 1) ? pc[i - 1] << 8 : 0u, false);
+    }
+    XcCls r;
+    r.C = (pc[1] << 15) | (pc[3] >> 1);
+    r.V = __builtin_amdgcn_udot4(z[1], xc_nl_weights(1), __builtin_amdgcn_udot4(z[0], xc_nl_weights(0), 0u, false),
+                                 false) +
+          __builtin_amdgcn_udot4(z[3], xc_nl_weights(3), __builtin_amdgcn_udot4(z[2], xc_nl_weights(2), 0u, false),
+                                 false);
+    return r;
+}
+
+// A region's window register after the newline entry is removed: the lane's 16 - nl
+// entries, lane L-1's entries (lane 0: ctx, the previous region's lane 63) above
+// them.  ctx and the result hold raw codes.
+struct XcWin {
+    uint32_t w0, w1, c, nl;
+};
+__device__ __forceinline__ XcWin xc_window(const XcCls& k, uint32_t ctx) {
+    uint32_t nl;   // min(V, 1), opaque (see x_window)
+    asm("v_min_u32_e32 %0, 1, %1" : "=v"(nl) : "v"(k.V));
+    const uint32_t q = min(k.V - 34u, 32u);   // 2e; no newline: wraps high, 32
+    const uint32_t L = (uint32_t)(~0ull << q);
+    const uint32_t c = bfi(L, k.C >> 2, k.C);
+    const uint32_t pC = wave_shr1(ctx, c);
+    const uint64_t t = (uint64_t)pC << (32u - 2u * nl);
+    XcWin x;
+    x.w0 = c | (uint32_t)t, x.w1 = (uint32_t)(t >> 32), x.c = c, x.nl = nl;
+    return x;
+}
+
+// k = 7 adds of one region: pair j = windows 2j (newer) and 2j+1, the 8-mer at bits
+// [4j, 4j+16) of W; with a newline window 14 is left alone and goes to S.
+__device__ __forceinline__ void xc_pairs7(const XcWin& x, uint32_t (&rt)[8]) {
+    constexpr uint32_t PM = 0x1FFFCu;
+    const uint32_t one = 1u;
+    const uint32_t x0 = x.w0 << 1, x1 = __builtin_amdgcn_alignbit(x.w1, x.w0, 31);
+    const uint32_t y0 = __builtin_amdgcn_alignbit(x1, x0, 16);
+    const uint32_t H0 = (x.w0 << 4) & 0x10101010u, H1 = x.w0 & 0x10101010u;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+        const uint32_t a = ((j < 4 ? x0 : y0) >> (4 * (j & 3))) & PM;
+        const uint32_t H = (j & 1) ? H1 : H0;
+        uint32_t dl;
+        switch (j >> 1) {
+        case 0: dl = shl1_byte<0>(H, one); break;
+        case 1: dl = shl1_byte<1>(H, one); break;
+        case 2: dl = shl1_byte<2>(H, one); break;
+        default: dl = shl1_byte<3>(H, one); break;
+        }
+        rt[j] = lds_add_rtn(a, dl);
+    }
+    const uint32_t v = y0 >> 12;
+    const uint32_t a7 = bfi(0u - x.nl, kPBytes | (v & 0x7FFCu), v & PM);
+    rt[7] = lds_add_rtn(a7, shl1_byte<3>(H1, one));
+}
+
+// k = 8 adds of one region: window r = the 8-mer at bits [2r, 2r+16) of W, r < 16 - nl.
+__device__ __forceinline__ void xc_wins8(const XcWin& x, uint32_t (&rt)[16]) {
+    constexpr uint32_t PM = 0x1FFFCu;
+    const uint32_t one = 1u;
+    const uint32_t x0 = x.w0 << 1, x1 = __builtin_amdgcn_alignbit(x.w1, x.w0, 31);
+    const uint32_t y0 = __builtin_amdgcn_alignbit(x1, x0, 16);
+    const uint32_t keep15 = x.nl - 1u;   // 0 with a newline: window 15 is lane L-1's window 0
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t a = ((r < 8 ? x0 : y0) >> (2 * (r & 7))) & PM;
+        const int tb = r & 3;   // W bit 2r sits at bit 8m + 2tb of w0 (m = r >> 2): move it to 8m + 4
+        const uint32_t H = (tb == 0 ? x.w0 << 4 : (tb == 1 ? x.w0 << 2 : (tb == 2 ? x.w0 : x.w0 >> 2))) & 0x10101010u;
+        uint32_t dl;
+        switch (r >> 2) {
+        case 0: dl = shl1_byte<0>(H, one); break;
+        case 1: dl = shl1_byte<1>(H, one); break;
+        case 2: dl = shl1_byte<2>(H, one); break;
+        default: dl = shl1_byte<3>(H, one); break;
+        }
+        if (r == 15) dl &= keep15;
+        rt[r] = lds_add_rtn(a, dl);
+    }
+}
+
+// Fast case of a coalesced 3 KiB iteration (as x_fast): every region of every lane
+// is bases with at most one newline and the carry is complete.  u16 exactness as
+// x_fast: k = 7 adds 24 per lane and iteration, k = 8 48.
+template <int K>
+__device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
+                                        uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
+    constexpr uint32_t HOT = K == 8 ? kHot8 : kHot7;
+    constexpr uint32_t TM = (1u << (2 * (K - 1))) - 1u;
+    const XcCls k0 = xc_cls(d.q[0]), k1 = xc_cls(d.q[1]), k2 = xc_cls(d.q[2]);
+    carry = __builtin_amdgcn_readfirstlane(carry);
+    if (t_n(carry) < (uint32_t)(K - 1) || __builtin_amdgcn_ballot_w64(max(max(k0.V, k1.V), k2.V) >= kXcBad) != 0)
+        return false;
+    uint32_t o = 0;
+    const XcWin x0 = xc_window(k0, t_codes(carry));
+    const XcWin x1 = xc_window(k1, (uint32_t)__builtin_amdgcn_readlane((int)x0.c, kWave - 1) & TM);
+    const XcWin x2 = xc_window(k2, (uint32_t)__builtin_amdgcn_readlane((int)x1.c, kWave - 1) & TM);
+    if constexpr (K == 7) {
+        const XcWin* xs[3] = {&x0, &x1, &x2};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            uint32_t r[8];
+            xc_pairs7(*xs[i], r);
+#pragma unroll
+            for (int j = 0; j < 8; j += 4) o |= r[j] | r[j + 1] | r[j + 2] | r[j + 3];
+        }
+    } else {
+        const XcWin* xs[3] = {&x0, &x1, &x2};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            uint32_t r[16];
+            xc_wins8(*xs[i], r);
+#pragma unroll
+            for (int j = 0; j < 16; j += 4) o |= r[j] | r[j + 1] | r[j + 2] | r[j + 3];
+        }
+    }
+    lane_total -= x0.nl + x1.nl + x2.nl;   // + 48 per fast iteration, added by the caller
+    carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)x2.c, kWave - 1) & TM, 31u, 31u);
+    if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
+        x_scan_drain<K>(A.code2col, gcounts, lane);
+        drained = 1;
+    }
+    return true;
+}
+
 // Fast case of a 3 KiB iteration (uniform): every lane's 48 bytes are bases with
 // at most one newline, and the carry is complete; returns false (nothing
 // counted) otherwise.  u16 exactness: every add's return is checked at the end
@@ -565,8 +739,11 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
     Range rg;
     rg.init(glo, ghi, lo, hi);
     XBlock buf[kXRing];
+    auto load = [&](uint32_t r) {
+        return KF_XC ? xc_load(A.bytes, rg.c0, r, rg.end_r, lane) : x_load(A.bytes, rg.c0, r, rg.end_r, lane);
+    };
 #pragma unroll
-    for (int j = 0; j < kXRing; ++j) buf[j] = x_load(A.bytes, rg.c0, j * kXChunk, rg.end_r, lane);
+    for (int j = 0; j < kXRing; ++j) buf[j] = load(j * kXChunk);
     const uint32_t nx = (rg.nch + 2) / 3;   // 3 KiB iterations
     rg.warm16<K>(A, lane);
     __builtin_amdgcn_s_setprio(0);   // (the setup ran at top priority, see k1x_kernel)
@@ -578,7 +755,9 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
     auto step = [&](const XBlock& bf) {
         // one test for the whole 3 KiB (range edges, excluded intervals)
         bool fast = !rg.masked_span(A, rel, kXChunk);
-        if (fast) fast = x_fast<K>(bf, A, lane, carry, gcounts, lane_total, drained);
+        if (fast)
+            fast = KF_XC ? xc_fast<K>(bf, A, lane, carry, gcounts, lane_total, drained)
+                         : x_fast<K>(bf, A, lane, carry, gcounts, lane_total, drained);
         nfast += fast ? 1u : 0u;
         if (!fast) {
             // interval cursor before each 1 KiB third (a later test may advance it)
@@ -594,7 +773,8 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
                 if (h > 0 && r >= rg.nch * kChunk) break;
                 const bool mh = h == 0 ? m0 : (h == 1 ? m1 : m2);
                 const uint64_t ivh = h == 0 ? iv0 : (h == 1 ? iv1 : rg.iv);
-                const uint4 hb = rg.load(A.bytes, r, lane);
+                // the coalesced block already holds this third in the 16-byte lane layout
+                const uint4 hb = KF_XC ? bf.q[h] : rg.load(A.bytes, r, lane);
                 if (mh)
                     carry = x_singles<K, true>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
                 else
@@ -607,7 +787,7 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
 #pragma unroll
         for (int j = 0; j < kXRing; ++j) {
             step(buf[j]);
-            buf[j] = x_load(A.bytes, rg.c0, rel + (kXRing - 1) * kXChunk, rg.end_r, lane);
+            buf[j] = load(rel + (kXRing - 1) * kXChunk);
         }
     }
     const uint32_t rem = nx % kXRing;
