@@ -564,23 +564,33 @@ __device__ __forceinline__ XcCls xc_cls(const uint4 d) {
     return r;
 }
 
-// A region's window register after the newline entry is removed: the lane's 16 - nl
-// entries, lane L-1's entries (lane 0: ctx, the previous region's lane 63) above
-// them.  ctx and the result hold raw codes.
+// A region's window register W after the newline entry is removed: the lane's
+// 16 - nl entries c, lane L-1's entries pC above them (lane 0: lane 63 of the
+// previous region, passed as `rot`, a register whose lane 0 holds it).  Returned
+// as two views of X = W << 1: x0 = X bits 0..31, y0 = X bits 16..47 (pair and
+// window addresses are plain shifts and masks of them), c (for the half masks,
+// W bits 0..31 where they are read) and nl.
 struct XcWin {
-    uint32_t w0, w1, c, nl;
+    uint32_t x0, y0, c, nl;
 };
-__device__ __forceinline__ XcWin xc_window(const XcCls& k, uint32_t ctx) {
+__device__ __forceinline__ XcWin xc_window(const XcCls& k, uint32_t rot) {
     uint32_t nl;   // min(V, 1), opaque (see x_window)
     asm("v_min_u32_e32 %0, 1, %1" : "=v"(nl) : "v"(k.V));
     const uint32_t q = min(k.V - 34u, 32u);   // 2e; no newline: wraps high, 32
     const uint32_t L = (uint32_t)(~0ull << q);
     const uint32_t c = bfi(L, k.C >> 2, k.C);
-    const uint32_t pC = wave_shr1(ctx, c);
-    const uint64_t t = (uint64_t)pC << (32u - 2u * nl);
+    const uint32_t pC = wave_shr1(rot, c);
+    // W = c | pC << (32 - 2 nl) (64-bit), so X = W << 1 has
+    // x0 = c << 1 | (nl ? pC << 31 : 0), y0 = c >> 15 | pC << (17 - 2 nl)
     XcWin x;
-    x.w0 = c | (uint32_t)t, x.w1 = (uint32_t)(t >> 32), x.c = c, x.nl = nl;
+    x.x0 = (c << 1) | ((pC << 31) & (0u - nl));
+    x.y0 = (c >> 15) | (pC << (17u - 2u * nl));
+    x.c = c, x.nl = nl;
     return x;
+}
+// wave_ror:1 (lane 0 gets lane 63)
+__device__ __forceinline__ uint32_t wave_ror1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);
 }
 
 // k = 7 adds of one region: pair j = windows 2j (newer) and 2j+1, the 8-mer at bits
@@ -588,9 +598,8 @@ __device__ __forceinline__ XcWin xc_window(const XcCls& k, uint32_t ctx) {
 __device__ __forceinline__ void xc_pairs7(const XcWin& x, uint32_t (&rt)[8]) {
     constexpr uint32_t PM = 0x1FFFCu;
     const uint32_t one = 1u;
-    const uint32_t x0 = x.w0 << 1, x1 = __builtin_amdgcn_alignbit(x.w1, x.w0, 31);
-    const uint32_t y0 = __builtin_amdgcn_alignbit(x1, x0, 16);
-    const uint32_t H0 = (x.w0 << 4) & 0x10101010u, H1 = x.w0 & 0x10101010u;
+    const uint32_t x0 = x.x0, y0 = x.y0;
+    const uint32_t H0 = (x.c << 4) & 0x10101010u, H1 = x.c & 0x10101010u;
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
         const uint32_t a = ((j < 4 ? x0 : y0) >> (4 * (j & 3))) & PM;
@@ -613,14 +622,13 @@ __device__ __forceinline__ void xc_pairs7(const XcWin& x, uint32_t (&rt)[8]) {
 __device__ __forceinline__ void xc_wins8(const XcWin& x, uint32_t (&rt)[16]) {
     constexpr uint32_t PM = 0x1FFFCu;
     const uint32_t one = 1u;
-    const uint32_t x0 = x.w0 << 1, x1 = __builtin_amdgcn_alignbit(x.w1, x.w0, 31);
-    const uint32_t y0 = __builtin_amdgcn_alignbit(x1, x0, 16);
+    const uint32_t x0 = x.x0, y0 = x.y0, w0 = x.c;
     const uint32_t keep15 = x.nl - 1u;   // 0 with a newline: window 15 is lane L-1's window 0
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const uint32_t a = ((r < 8 ? x0 : y0) >> (2 * (r & 7))) & PM;
         const int tb = r & 3;   // W bit 2r sits at bit 8m + 2tb of w0 (m = r >> 2): move it to 8m + 4
-        const uint32_t H = (tb == 0 ? x.w0 << 4 : (tb == 1 ? x.w0 << 2 : (tb == 2 ? x.w0 : x.w0 >> 2))) & 0x10101010u;
+        const uint32_t H = (tb == 0 ? w0 << 4 : (tb == 1 ? w0 << 2 : (tb == 2 ? w0 : w0 >> 2))) & 0x10101010u;
         uint32_t dl;
         switch (r >> 2) {
         case 0: dl = shl1_byte<0>(H, one); break;
@@ -647,8 +655,8 @@ __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int
         return false;
     uint32_t o = 0;
     const XcWin x0 = xc_window(k0, t_codes(carry));
-    const XcWin x1 = xc_window(k1, (uint32_t)__builtin_amdgcn_readlane((int)x0.c, kWave - 1) & TM);
-    const XcWin x2 = xc_window(k2, (uint32_t)__builtin_amdgcn_readlane((int)x1.c, kWave - 1) & TM);
+    const XcWin x1 = xc_window(k1, wave_ror1(x0.c));
+    const XcWin x2 = xc_window(k2, wave_ror1(x1.c));
     if constexpr (K == 7) {
         const XcWin* xs[3] = {&x0, &x1, &x2};
 #pragma unroll
