@@ -246,11 +246,14 @@ __device__ __forceinline__ void apply_masks(const CountArgs& A, uint64_t chunk, 
 // num_records, so an exact (unaligned) end would drop the genome's last bases.
 // Bytes in [ghi, align16(ghi)) are read but never counted (they lie past hi).
 // c = c0 + rel; end_r = align16(ghi) - c0 (32-bit: see process_range)
+#ifndef KF_CHUNK_CPOL
+#define KF_CHUNK_CPOL 0   // buffer-load cache policy of the 1 KiB chunk stream (2 = nt)
+#endif
 __device__ __forceinline__ uint4 load_chunk(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r,
                                             int lane) {
     const uint32_t rec = end_r > rel ? min(end_r - rel, (uint32_t)kChunk) : 0u;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c0 + rel), (short)0, (int)rec, 0x00020000);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, KF_CHUNK_CPOL);
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
