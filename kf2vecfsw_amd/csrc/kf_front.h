@@ -247,7 +247,7 @@ __device__ __forceinline__ void apply_masks(const CountArgs& A, uint64_t chunk, 
 // Bytes in [ghi, align16(ghi)) are read but never counted (they lie past hi).
 // c = c0 + rel; end_r = align16(ghi) - c0 (32-bit: see process_range)
 #ifndef KF_CHUNK_CPOL
-#define KF_CHUNK_CPOL 0   // buffer-load cache policy of the 1 KiB chunk stream (2 = nt)
+#define KF_CHUNK_CPOL 2   // 1 KiB chunk stream: non-temporal (k=5 -1.3 %, k=9 -1.7 %, k=11 same; v10_lib_ab_*_chunk_nt)
 #endif
 __device__ __forceinline__ uint4 load_chunk(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r,
                                             int lane) {
