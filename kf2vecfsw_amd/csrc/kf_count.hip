@@ -45,7 +45,10 @@ constexpr int kBlock = 1024;             // threads per workgroup, both kernels
 constexpr int kWaves = kBlock / kWave;   // 16
 // K1x: a genome piece's share per wave by the wave's age slot on its SIMD (the
 // SIMD issues oldest-first; slot 0 runs ~2.4x faster than slot 3), 8 bits each
-constexpr uint32_t kWaveWeights = 20u | 17u << 8 | 11u << 16 | 6u << 24;
+#ifndef KF_WAVE_WEIGHTS
+#define KF_WAVE_WEIGHTS (20u | 17u << 8 | 11u << 16 | 6u << 24)
+#endif
+constexpr uint32_t kWaveWeights = KF_WAVE_WEIGHTS;
 constexpr int kK1Ring = 4;   // K1: 1 KiB chunks in the register ring
 constexpr int kXRing = 2;    // K1x: 3 KiB iterations in the register ring
 
@@ -515,6 +518,9 @@ __device__ __forceinline__ uint32_t x_body8(const XCls& k, uint32_t& carry, uint
 #ifndef KF_XC
 #define KF_XC 1
 #endif
+#ifndef KF_NT_STORES
+#define KF_NT_STORES 1   // non-temporal count-row stores (k=7 -1.4 %; v10_lib_ab_k*_nt_stores)
+#endif
 constexpr int kXNt = 2;   // buffer-load cache policy bit: non-temporal
 
 __device__ __forceinline__ XBlock xc_load(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r, int lane) {
@@ -934,8 +940,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 
             // the row writes last: their issue overlaps the zeroing, the barrier
             // and the next piece's setup
             if (whole && !any_drain) {
+#if KF_NT_STORES
+                typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(v4u_t{cv[0], cv[1], cv[2], cv[3]}, (v4u_t*)(gc + 4 * tid));
+                __builtin_nontemporal_store(v4u_t{cv[4], cv[5], cv[6], cv[7]}, (v4u_t*)(gc + 4096 + 4 * tid));
+#else
                 *(uint4*)(gc + 4 * tid) = make_uint4(cv[0], cv[1], cv[2], cv[3]);
                 *(uint4*)(gc + 4096 + 4 * tid) = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+#endif
             } else {
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
