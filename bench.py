@@ -182,8 +182,8 @@ def load_traffic(k: int, workload_tag: str):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--k", type=int, default=7)
     ap.add_argument("--workload", choices=["auto", "configs1", "configs3"], default="auto",
                     help="auto: configs1 (1,000 genomes per GPU) at N=1, configs3 (50,000 genomes sharded) at N>1")
