@@ -156,6 +156,14 @@ __device__ __forceinline__ uint32_t rec_addr(uint32_t d, int h) {
             : "=v"(r) : "v"(d));
     return r;
 }
+// v_bfe_u32 the compiler cannot take apart: (bfe(s) << n) + base then stays one
+// v_lshl_add / v_lshl_or instead of lshr + and + add.
+template <int OFF, int W>
+__device__ __forceinline__ uint32_t bfe_opaque(uint32_t s) {
+    uint32_t r;
+    asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(r) : "v"(s), "i"(OFF), "i"(W));
+    return r;
+}
 __device__ __forceinline__ uint32_t lds_ld(uint32_t a) { return *(volatile lds_u32*)(uintptr_t)a; }
 __device__ __forceinline__ void lds_st(uint32_t a, uint32_t v) { *(volatile lds_u32*)(uintptr_t)a = v; }
 typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
@@ -235,8 +243,9 @@ __global__ void __launch_bounds__(256) zero_split_rows_kernel(const uint64_t* go
 // Canonical lexicographic codes of the 16 windows of a lane (kf codes in W).
 // std code = kf ^ ((kf >> 1) & 0x55..) per base (A0 C1 T2 G3 -> A0 C1 G2 T3);
 // complement in std code = code ^ 3, so the reversed complement of the whole
-// 64-bit window register is ~revpairs, word-swapped.
-template <int K>
+// 64-bit window register is ~revpairs, word-swapped.  DENSE (fast_windows):
+// windows 0..14 are valid by construction, so only window 15 is tested.
+template <int K, bool DENSE = false>
 __device__ __forceinline__ void canon_std(const Windows& w, uint32_t (&s)[16]) {
     constexpr int W2 = 2 * K;
     const uint32_t slo = w.wlo ^ ((w.wlo >> 1) & 0x55555555u);
@@ -254,7 +263,7 @@ __device__ __forceinline__ void canon_std(const Windows& w, uint32_t (&s)[16]) {
         const uint32_t f = __builtin_amdgcn_ubfe(fv[fo >> 3], 2 * r - fo, W2);
         const int rr = 2 * (15 - r), ro = rr & ~7;
         const uint32_t c = __builtin_amdgcn_ubfe(rv[ro >> 3], rr - ro, W2);
-        s[r] = ((w.R >> r) & 1u) ? min(f, c) : 0xFFFFFFFFu;
+        s[r] = ((DENSE && r < 15) || ((w.R >> r) & 1u)) ? min(f, c) : 0xFFFFFFFFu;
     }
 }
 
@@ -348,7 +357,10 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         const uint32_t rb = L::rbase + (uint32_t)wave * L::tbl_bytes;
         // byte offset of the rank entry of canonical code s for this lane (its replica)
         const uint32_t repo = ((uint32_t)lane & (L::nrep - 1u)) << 2;
-        auto ent = [&](uint32_t s) -> uint32_t { return ((s >> kBkBits) << (L::rl + 2)) | repo; };
+        // bucket part of the entry offset (one bfe; the lshl folds into the
+        // address op): a counter set base is 4 nent aligned, so `cb | ent` = cb + ent
+        auto ent_b = [&](uint32_t s) -> uint32_t { return bfe_opaque<kBkBits, 2 * K - kBkBits>(s) << (L::rl + 2); };
+        static_assert((L::cnt % (4 * L::nent)) == 0, "counter sets are 4 nent aligned");
         auto copy_out = [&](uint32_t r, uint32_t T, uint32_t o) {
             const uint32_t st = L::stage + (r & 1) * L::stage_bytes;
             for (uint32_t q = tid; q < T / 8; q += kBkBlock) {
@@ -363,6 +375,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         auto round = [&](uint32_t r, uint4& bf) {
             const uint32_t cb = L::cnt + 4 * L::nent * (r % 3);
             const uint32_t cz = L::cnt + 4 * L::nent * ((r + 1) % 3);
+            const uint32_t cbr = cb | repo;   // rank address of s: cbr | ent_b(s)
             for (uint32_t e = tid; e < L::nent; e += kBkBlock) lds_st(cz + 4 * e, 0u);
             uint32_t s[16], rk[16];
             const bool have = r < nch;
@@ -376,19 +389,19 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                     // newline; ranks without per-record branches
                     dense = true;
                     carry = w.next;
-                    canon_std<K>(w, s);
+                    canon_std<K, true>(w, s);
 #pragma unroll
 #if KF_BK_ABL == 3   // profiling only: no rank atomics (ranks by lane: wrong counts)
                     for (int j = 0; j < 15; ++j) rk[j] = (uint32_t)lane * 16 + j;
 #elif KF_BK_ABL == 7   // profiling only: rank adds without returns (ranks by lane: wrong counts)
                     for (int j = 0; j < 15; ++j) {
-                        lds_add(cb + ent(s[j]), 1u);
+                        lds_add(cbr | ent_b(s[j]), 1u);
                         rk[j] = (uint32_t)lane * 16 + j;
                     }
 #else
-                    for (int j = 0; j < 15; ++j) rk[j] = lds_add_rtn(cb + ent(s[j]), 1u);
+                    for (int j = 0; j < 15; ++j) rk[j] = lds_add_rtn(cbr | ent_b(s[j]), 1u);
 #endif
-                    if (s[15] != 0xFFFFFFFFu) rk[15] = lds_add_rtn(cb + ent(s[15]), 1u);
+                    if (s[15] != 0xFFFFFFFFu) rk[15] = lds_add_rtn(cbr | ent_b(s[15]), 1u);
                 } else {
                     uint32_t C, V, EN, ne, own;
                     if (msk) {
@@ -402,7 +415,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                     canon_std<K>(w, s);
 #pragma unroll
                     for (int j = 0; j < 16; ++j)
-                        if (s[j] != 0xFFFFFFFFu) rk[j] = lds_add_rtn(cb + ent(s[j]), 1u);
+                        if (s[j] != 0xFFFFFFFFu) rk[j] = lds_add_rtn(cbr | ent_b(s[j]), 1u);
                 }
                 rel += kChunk;
                 if (rel + 3 * kChunk < nch * kChunk) bf = rg.load(A.bytes, rel + 3 * kChunk, lane);
@@ -505,28 +518,32 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                             *(volatile lds_u16*)(uintptr_t)(st + 2 * (e + x)) = (uint16_t)(kSentinel | ((e + x) & 63u));
                 }
             }
+            // Staging: every table read is issued before the first record write
+            // (a read after a write would wait for the write's round trip: the
+            // accesses are volatile, so the compiler keeps their order).
+            const uint32_t rbr = rb + repo;
             if (dense) {
 #pragma unroll
+                for (int j = 0; j < 15; ++j) rk[j] += lds_ld(rbr + ent_b(s[j]));
+                if (s[15] != 0xFFFFFFFFu) rk[15] += lds_ld(rbr + ent_b(s[15]));
+#pragma unroll
                 for (int j = 0; j < 15; ++j) {
-                    const uint32_t slot = lds_ld(rb + ent(s[j])) + rk[j];
 #if KF_BK_ABL == 4   // profiling only: no staging writes (wrong counts)
-                    asm volatile("" ::"v"(slot), "v"(s[j]));
+                    asm volatile("" ::"v"(rk[j]), "v"(s[j]));
 #else
-                    *(volatile lds_u16*)(uintptr_t)(st + 2 * slot) = (uint16_t)(s[j] & (kBkCodes - 1));
+                    *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[j]) = (uint16_t)(s[j] & (kBkCodes - 1));
 #endif
                 }
-                if (s[15] != 0xFFFFFFFFu) {
-                    const uint32_t slot = lds_ld(rb + ent(s[15])) + rk[15];
-                    *(volatile lds_u16*)(uintptr_t)(st + 2 * slot) = (uint16_t)(s[15] & (kBkCodes - 1));
-                }
+                if (s[15] != 0xFFFFFFFFu)
+                    *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[15]) = (uint16_t)(s[15] & (kBkCodes - 1));
             } else if (have) {
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    if (s[j] != 0xFFFFFFFFu) {
-                        const uint32_t slot = lds_ld(rb + ent(s[j])) + rk[j];
-                        *(volatile lds_u16*)(uintptr_t)(st + 2 * slot) = (uint16_t)(s[j] & (kBkCodes - 1));
-                    }
-                }
+                for (int j = 0; j < 16; ++j)
+                    if (s[j] != 0xFFFFFFFFu) rk[j] += lds_ld(rbr + ent_b(s[j]));
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (s[j] != 0xFFFFFFFFu)
+                        *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[j]) = (uint16_t)(s[j] & (kBkCodes - 1));
             }
             t_prev = T;
             off_prev = off;
