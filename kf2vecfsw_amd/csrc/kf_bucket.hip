@@ -48,24 +48,58 @@ namespace kf {
 #ifndef KF_BK_DB
 #define KF_BK_DB 1
 #endif
+// With KF_BK_DB, k <= 10: both groups of the next bucket are issued before the
+// current bucket's flush, so its first two groups never wait for loads issued
+// after the flush (one process: k=9 6.10 -> 5.83 ms, k=10 6.71 -> 6.52).  k >= 11
+// issues one: k=11 buckets need ~1.2 groups per wave (8.69 vs 8.73 ms) and k=12
+// ~0.3 (18.9 vs 19.2), so a second group is mostly empty loads.
+#ifndef KF_BK_PRE2
+#define KF_BK_PRE2 1
+#endif
 // Non-temporal stores for the record copy-out and the count rows: k=11 9.61 ->
 // 8.97 ms, k=9 unchanged (one process, profiles/r03/v10_lib_ab_k*_nt_stores.json).
 #ifndef KF_NT_STORES
 #define KF_NT_STORES 1
 #endif
 
-constexpr int kBkBits = 15;                          // 32768 codes per bucket
-constexpr uint32_t kBkCodes = 1u << kBkBits;
-constexpr int kBkWaves = 16;
-constexpr int kBkBlock = kBkWaves * kWave;
-constexpr uint32_t kRoundRecs = kBkWaves * kChunk;   // windows per round (<= 16384)
-constexpr uint64_t kPieceMax = 8ull << 20;           // bytes per piece (one workgroup)
-// rounds per piece: a wave range is <= piece/16 + 16 bytes, i.e. <= 513 chunks
-constexpr uint32_t kRmax = (uint32_t)(kPieceMax / kRoundRecs) + 2;
-// A record is s & 0x7FFF.  Runs (one bucket, one round) are padded to whole
-// 8-record units with sentinels 0x8000 | x, which phase 2 counts into a trash
+// Workgroup shape (per k, compile time): W = 16 waves, one workgroup per CU,
+// 32768-code buckets (a 128 KiB histogram); or W = 8 waves, two workgroups per
+// CU, 16384-code buckets (64 KiB), so that one workgroup's barrier waits are
+// filled by the other's waves and the two phases of different pieces overlap on
+// one CU.  KF_BK_W<k> (tools/ A/B builds):
+#ifndef KF_BK_W9
+#define KF_BK_W9 16
+#endif
+#ifndef KF_BK_W10
+#define KF_BK_W10 16
+#endif
+#ifndef KF_BK_W11
+#define KF_BK_W11 16
+#endif
+constexpr int bk_w(int K) { return K == 9 ? KF_BK_W9 : K == 10 ? KF_BK_W10 : K == 11 ? KF_BK_W11 : 16; }
+// bytes per piece (one workgroup): a wave range is <= piece / W + 16 bytes, so
+// <= 1017 rounds at W = 8 (<= 128 phase-2 runs per wave, two per lane) and <= 509
+// at W = 16
+constexpr uint64_t kPieceMax = (8ull << 20) - (64ull << 10);
+template <int W>
+struct BkGeom {
+    static_assert(W == 8 || W == 16, "8 or 16 waves");
+    static constexpr int waves = W;
+    static constexpr int block = W * kWave;
+    static constexpr int bits = W == 16 ? 15 : 14;                        // code bits per bucket
+    static constexpr uint32_t codes = 1u << bits;
+    static constexpr uint32_t round_recs = W * kChunk;                   // windows per round
+    static constexpr uint32_t rmax = (uint32_t)(kPieceMax / round_recs) + 2;   // rounds per piece
+    static constexpr int halves = (rmax + W * kWave - 1) / (W * kWave);   // phase-2 runs per lane
+    static_assert(halves <= 2, "phase-2 run tables hold two runs per lane");
+};
+// A record is the low 16 bits of s: its code in the bucket (s mod codes) plus the
+// bucket's low 16 - bits bits (the same for a whole bucket; phase 1 stores s as
+// it is, one op less per window).  Runs (one bucket, one round) are padded to
+// whole 8-record units with sentinels x | ((b ^ 1) mod 2^(16-bits)) << bits
+// (x < 64).  Phase 2 XORs each record with bucket b's high part (b mod
+// 2^(16-bits)) << bits: records become s mod codes, sentinels codes + x, a trash
 // area past the histogram, so a 16-byte unit never needs a range test.
-constexpr uint32_t kSentinel = 0x8000u;
 
 // Phase-1 rank counters: each bucket's round counter is split into R = 2^rl
 // lane replicas (lane L ranks into replica L mod R), so the 64 lanes of one
@@ -93,16 +127,18 @@ constexpr uint32_t bk_rl(int K) {
     return K == 9 ? KF_BK_RL9 : K == 10 ? KF_BK_RL10 : K == 11 ? KF_BK_RL11 : KF_BK_RL12;
 }
 
-template <int K>
-struct Bk {
-    static constexpr uint32_t nbk = (1u << (2 * K)) >> kBkBits;   // buckets
-    static constexpr uint32_t rl = bk_rl(K);
+template <int K, int W = bk_w(K)>
+struct Bk : BkGeom<W> {
+    using G = BkGeom<W>;
+    static constexpr uint32_t nbk = (1u << (2 * K)) >> G::bits;   // buckets
+    // (W = 8: twice the buckets, half the replicas: the same counter count)
+    static constexpr uint32_t rl = W == 16 || bk_rl(K) == 0 ? bk_rl(K) : bk_rl(K) - 1;
     static constexpr uint32_t nrep = 1u << rl;                      // rank replicas per bucket
     static constexpr uint32_t nent = nbk << rl;                     // rank entries per round
     static constexpr uint32_t epl = nent / kWave;                   // rank entries per lane
-    static constexpr uint32_t round_cap = kRoundRecs + 7 * nbk;     // records of a padded round
-    static constexpr uint64_t rec_cap = (uint64_t)kRmax * round_cap + 8;   // per workgroup
-    // LDS byte layout.  Phase 2: the 128 KiB histogram at 0.  Phase 1 reuses it:
+    static constexpr uint32_t round_cap = G::round_recs + 7 * nbk;  // records of a padded round
+    static constexpr uint64_t rec_cap = (uint64_t)G::rmax * round_cap + 8;   // per workgroup
+    // LDS byte layout.  Phase 2: the histogram (codes u32) at 0.  Phase 1 reuses it:
     // two round staging buffers, then one private rank-entry offset table per
     // wave.  After the histogram: three rotating sets of round rank counters
     // (phase 1), which phase 2 reuses as the sentinels' trash bins, and the
@@ -112,26 +148,26 @@ struct Bk {
     static constexpr uint32_t stage = 0;                            // + (r & 1) * stage_bytes
     static constexpr uint32_t tbl_bytes = nent * 4 + 16;            // per wave (16-byte aligned)
     static constexpr uint32_t rbase = 2 * stage_bytes;              // + wave * tbl_bytes
-    static constexpr uint32_t dirty = rbase + kBkWaves * tbl_bytes;   // phase-1 footprint in hist
-    static constexpr uint32_t cnt = kBkCodes * 4;                   // + (r % 3) * nent * 4
-    static constexpr uint32_t red = (cnt + 3 * nent * 4 + 7) & ~7u; // kBkWaves u64
+    static constexpr uint32_t dirty = rbase + W * tbl_bytes;       // phase-1 footprint in hist
+    static constexpr uint32_t cnt = G::codes * 4;                   // + (r % 3) * nent * 4
+    static constexpr uint32_t red = (cnt + 3 * nent * 4 + 7) & ~7u; // W u64
     static constexpr uint32_t lds_bytes =
-        red + kBkWaves * 8 > cnt + 256 ? red + kBkWaves * 8 : cnt + 256;   // trash: 64 bins at cnt
+        red + W * 8 > cnt + 256 ? red + W * 8 : cnt + 256;         // trash: 64 bins at cnt
+    static constexpr uint32_t hmask = (1u << (16 - G::bits)) - 1u;  // bucket bits inside a record
     static_assert(epl >= 1 && epl <= 8 && (epl & (epl - 1)) == 0 && nent == epl * kWave, "1-8 entries per lane");
-    static_assert(dirty <= kBkCodes * 4, "phase-1 tables must fit the histogram area");
-    static_assert(lds_bytes <= 160 * 1024, "LDS");
+    static_assert(dirty <= G::codes * 4, "phase-1 tables must fit the histogram area");
+    static_assert(lds_bytes * (16 / W) <= 160 * 1024, "LDS (16 / W workgroups per CU)");
     static_assert(round_cap < 65536, "round offsets are u16");
 };
 
 struct BucketArgs {
-    const uint16_t* col_idx;   // nbins: canonical code & 0x7FFF per column
+    const uint16_t* col_idx;   // nbins: canonical code mod codes per column
     const uint32_t* bcol;      // nbk+1: first column of each bucket
     const uint32_t* pstart;    // n_genomes+1: first piece of each genome
     uint16_t* rec;             // gridDim.x * Bk<K>::rec_cap records
-    uint16_t* meta;            // gridDim.x * (nbk+1) * kRmax round bucket offsets
-    uint32_t* roff;            // gridDim.x * kRmax round record offsets
+    uint16_t* meta;            // gridDim.x * (nbk+1) * rmax round bucket offsets
+    uint32_t* roff;            // gridDim.x * rmax round record offsets
     uint32_t accumulate;
-    uint32_t slot_w;            // phase-2 rounds per wave by wave slot (4 x 8 bit, see bucket_weights)
     unsigned long long* prof;   // optional (KF_BUCKET_PROFILE): per-workgroup phase cycles
 };
 
@@ -297,20 +333,22 @@ __device__ __forceinline__ bool fast_windows(const uint4 d, uint32_t carry, Wind
 }
 
 template <int K>
-__global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArgs B) {
+__global__ void __launch_bounds__(Bk<K>::block) __attribute__((amdgpu_waves_per_eu(4, 4)))   // 16 waves per CU
+bucket_kernel(CountArgs A, BucketArgs B) {
     using L = Bk<K>;
+    constexpr int W = L::waves;
     constexpr uint32_t NBK = L::nbk;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if ((uint32_t)(uintptr_t)(lds_u32*)lds != 0u) __builtin_trap();   // raw LDS addresses assume base 0
-    for (uint32_t i = tid; i < kBkCodes + NBK; i += kBkBlock) lds[i] = 0;   // histogram + counters
+    for (uint32_t i = tid; i < L::codes + NBK; i += L::block) lds[i] = 0;   // histogram + counters
     __syncthreads();
 
     uint16_t* rec = B.rec + (uint64_t)blockIdx.x * L::rec_cap;
-    uint16_t* meta = B.meta + (uint64_t)blockIdx.x * (NBK + 1) * kRmax;
-    uint32_t* roff = B.roff + (uint64_t)blockIdx.x * kRmax;
+    uint16_t* meta = B.meta + (uint64_t)blockIdx.x * (NBK + 1) * L::rmax;
+    uint32_t* roff = B.roff + (uint64_t)blockIdx.x * L::rmax;
     const uint32_t npiece = B.pstart[A.n_genomes];
 
     for (uint32_t p = blockIdx.x; p < npiece; p += gridDim.x) {
@@ -320,11 +358,11 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         const uint32_t np = B.pstart[g + 1] - B.pstart[g], pi = p - B.pstart[g];
         const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
         const uint64_t plo = split_at(glo, ghi, pi, np), phi = split_at(glo, ghi, pi + 1, np);
-        const uint64_t lo = split_at(plo, phi, wave, kBkWaves), hi = split_at(plo, phi, wave + 1, kBkWaves);
+        const uint64_t lo = split_at(plo, phi, wave, W), hi = split_at(plo, phi, wave + 1, W);
         // rounds = the longest wave range in chunks (same value in every wave)
         uint32_t nround = 0;
-        for (int w = 0; w < kBkWaves; ++w) {
-            const uint64_t a = split_at(plo, phi, w, kBkWaves), e = split_at(plo, phi, w + 1, kBkWaves);
+        for (int w = 0; w < W; ++w) {
+            const uint64_t a = split_at(plo, phi, w, W), e = split_at(plo, phi, w + 1, W);
             if (e > a) nround = max(nround, (uint32_t)((e - (a & ~(uint64_t)15) + kChunk - 1) / kChunk));
         }
 
@@ -349,7 +387,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         // computes the bucket offsets of round r into its private table (no
         // serial scan, no second barrier), and stages its records.  A counter set
         // is zeroed two rounds after its last read, so the barriers order it.
-        for (uint32_t i = tid; i < 3 * L::nent; i += kBkBlock) lds_st(L::cnt + 4 * i, 0u);
+        for (uint32_t i = tid; i < 3 * L::nent; i += L::block) lds_st(L::cnt + 4 * i, 0u);
         lds_barrier();
         uint64_t p1w = 0;                    // profile: phase-1 barrier wait of this wave
         uint32_t off = 0;                    // records of rounds before the current one (x8)
@@ -359,11 +397,11 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         const uint32_t repo = ((uint32_t)lane & (L::nrep - 1u)) << 2;
         // bucket part of the entry offset (one bfe; the lshl folds into the
         // address op): a counter set base is 4 nent aligned, so `cb | ent` = cb + ent
-        auto ent_b = [&](uint32_t s) -> uint32_t { return bfe_opaque<kBkBits, 2 * K - kBkBits>(s) << (L::rl + 2); };
+        auto ent_b = [&](uint32_t s) -> uint32_t { return bfe_opaque<L::bits, 2 * K - L::bits>(s) << (L::rl + 2); };
         static_assert((L::cnt % (4 * L::nent)) == 0, "counter sets are 4 nent aligned");
         auto copy_out = [&](uint32_t r, uint32_t T, uint32_t o) {
             const uint32_t st = L::stage + (r & 1) * L::stage_bytes;
-            for (uint32_t q = tid; q < T / 8; q += kBkBlock) {
+            for (uint32_t q = tid; q < T / 8; q += L::block) {
                 const v4u v = *(lds_v4u*)(uintptr_t)(st + 16 * q);
 #if KF_NT_STORES
                 __builtin_nontemporal_store(v, (v4u*)(rec + o + 8 * q));
@@ -376,7 +414,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             const uint32_t cb = L::cnt + 4 * L::nent * (r % 3);
             const uint32_t cz = L::cnt + 4 * L::nent * ((r + 1) % 3);
             const uint32_t cbr = cb | repo;   // rank address of s: cbr | ent_b(s)
-            for (uint32_t e = tid; e < L::nent; e += kBkBlock) lds_st(cz + 4 * e, 0u);
+            for (uint32_t e = tid; e < L::nent; e += L::block) lds_st(cz + 4 * e, 0u);
             uint32_t s[16], rk[16];
             const bool have = r < nch;
             bool dense = false;   // wave-uniform: windows 0..14 of every lane are valid (fast case)
@@ -499,23 +537,24 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             };
             if (wave == 0 && bown) {
 #pragma unroll
-                for (uint32_t q = 0; q < BPL; ++q) meta[(uint64_t)bid(q) * kRmax + r] = (uint16_t)bst[q];
+                for (uint32_t q = 0; q < BPL; ++q) meta[(uint64_t)bid(q) * L::rmax + r] = (uint16_t)bst[q];
             }
             if (wave == 0 && lane == kWave - 1) {
-                meta[(uint64_t)NBK * kRmax + r] = (uint16_t)T;
+                meta[(uint64_t)NBK * L::rmax + r] = (uint16_t)T;
                 roff[r] = off;
             }
             const uint32_t st = L::stage + (r & 1) * L::stage_bytes;
             // sentinels after each run, up to its unit boundary (one wave per
             // round, rotating)
-            if ((r % kBkWaves) == (uint32_t)wave && bown) {
+            if ((r % W) == (uint32_t)wave && bown) {
 #pragma unroll
                 for (uint32_t q = 0; q < BPL; ++q) {
                     const uint32_t e = bst[q] + bcnt[q], npad = (8u - (bcnt[q] & 7u)) & 7u;
 #pragma unroll
                     for (uint32_t x = 0; x < 7; ++x)
                         if (x < npad)
-                            *(volatile lds_u16*)(uintptr_t)(st + 2 * (e + x)) = (uint16_t)(kSentinel | ((e + x) & 63u));
+                            *(volatile lds_u16*)(uintptr_t)(st + 2 * (e + x)) =
+                                (uint16_t)((((bid(q) ^ 1u) & L::hmask) << L::bits) | ((e + x) & 63u));
                 }
             }
             // Staging: every table read is issued before the first record write
@@ -531,11 +570,11 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
 #if KF_BK_ABL == 4   // profiling only: no staging writes (wrong counts)
                     asm volatile("" ::"v"(rk[j]), "v"(s[j]));
 #else
-                    *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[j]) = (uint16_t)(s[j] & (kBkCodes - 1));
+                    *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[j]) = (uint16_t)s[j];
 #endif
                 }
                 if (s[15] != 0xFFFFFFFFu)
-                    *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[15]) = (uint16_t)(s[15] & (kBkCodes - 1));
+                    *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[15]) = (uint16_t)s[15];
             } else if (have) {
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
@@ -543,7 +582,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
                     if (s[j] != 0xFFFFFFFFu)
-                        *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[j]) = (uint16_t)(s[j] & (kBkCodes - 1));
+                        *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[j]) = (uint16_t)s[j];
             }
             t_prev = T;
             off_prev = off;
@@ -567,58 +606,72 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         // the stores, and read them with L1-bypassing loads below
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         const uint64_t t_p2 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
-        for (uint32_t i = tid; i < L::dirty / 4; i += kBkBlock) lds_st(L::hist + 4 * i, 0u);   // phase-1 area
+        for (uint32_t i = tid; i < L::dirty / 4; i += L::block) lds_st(L::hist + 4 * i, 0u);   // phase-1 area
         lds_barrier();
         uint32_t* row = A.counts + (uint64_t)g * A.nbins;
         const bool split = np > 1;
         unsigned long long tsum = 0;
-        // Run table of this wave: lane j (< nrun) <-> round wave + 16 j.  A run is
-        // the whole units of one bucket in one round (padded by phase 1), and the
-        // units of all the wave's runs are laid end to end (prefix P over lanes),
-        // so every load instruction carries 64 units whatever the run lengths.
-        // A group is kGW windows of 64 units (512 units: a whole k=11 bucket of a
-        // wave, typically); the next bucket's first group is issued before this
-        // bucket's flush, so its loads are in flight during the flush.  Loads are
-        // unconditional (inactive lanes read unit 0) so vmcnt stays exact.
-        // Rounds are dealt to waves in patterns of 4 (a0 + a1 + a2 + a3) rounds, a_s
-        // consecutive rounds to each wave of slot s = wave >> 2 (its age on its
-        // SIMD: older slots issue first and finish sooner, so they may take more);
-        // a = 1,1,1,1 is round wave + 16 j.  The valid runs are lanes 0 .. nrun-1.
-        const uint32_t slot = (uint32_t)wave >> 2;
-        const uint32_t a_s = (B.slot_w >> (8 * slot)) & 0xFFu;
-        const uint32_t a_below = ((B.slot_w & 0xFFu) * (slot > 0)) + (((B.slot_w >> 8) & 0xFFu) * (slot > 1)) +
-                                 (((B.slot_w >> 16) & 0xFFu) * (slot > 2));
-        const uint32_t per = 4 * ((B.slot_w & 0xFFu) + ((B.slot_w >> 8) & 0xFFu) + ((B.slot_w >> 16) & 0xFFu) +
-                                  (B.slot_w >> 24));
-        const uint32_t lq = (uint32_t)lane / a_s;
-        const uint32_t myr = lq * per + 4 * a_below + ((uint32_t)wave & 3u) * a_s + ((uint32_t)lane - lq * a_s);
-        const bool myr_ok = myr < nround;
-        const uint32_t myr_c = myr_ok ? myr : 0u;
-        const uint32_t nrun = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(myr_ok));
-        const uint32_t ro_l = __builtin_nontemporal_load(roff + myr_c);
-        const uint32_t ro = myr_ok ? ro_l : 0u;
+        // Run table of this wave: run j (< nrun) <-> round wave + W j, held by lane
+        // j mod 64 in half j / 64 (W = 8 needs up to 128 runs).  A run is the whole
+        // units of one bucket in one round (padded by phase 1), and the units of
+        // all the wave's runs are laid end to end (prefix P over the runs), so
+        // every load instruction carries 64 units whatever the run lengths.  A
+        // group is kGW windows of 64 units; the next bucket's first group is
+        // issued before this bucket's flush, so its loads are in flight during the
+        // flush.  Loads are unconditional (inactive lanes read unit 0) so vmcnt
+        // stays exact.
+        constexpr int H = L::halves;
+        bool myr_ok[H];
+        uint32_t myr_c[H], ro[H];
+        uint32_t nrun = 0;
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+            const uint32_t myr = (uint32_t)wave + (uint32_t)W * (64u * h + (uint32_t)lane);
+            myr_ok[h] = myr < nround;
+            myr_c[h] = myr_ok[h] ? myr : 0u;
+            nrun += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(myr_ok[h]));
+            const uint32_t ro_l = __builtin_nontemporal_load(roff + myr_c[h]);
+            ro[h] = myr_ok[h] ? ro_l : 0u;
+        }
+        struct Hv {
+            uint32_t v[H];
+        };
         // raw (lanes without a run read round 0; make_tbl masks them), so that
         // the load is not waited for until its table is built
-        auto meta_at = [&](uint32_t b) -> uint32_t {
-            return __builtin_nontemporal_load(meta + (uint64_t)b * kRmax + myr_c);
+        auto meta_at = [&](uint32_t b) -> Hv {
+            Hv m;
+#pragma unroll
+            for (int h = 0; h < H; ++h) m.v[h] = __builtin_nontemporal_load(meta + (uint64_t)b * L::rmax + myr_c[h]);
+            return m;
         };
         struct Tbl {
-            uint32_t P, DL;          // per lane (run): first unit in the bucket's unit space, unit delta
+            uint32_t P[H], DL[H];    // per run: first unit in the bucket's unit space, unit delta
             uint32_t U, jn, cur, w0; // wave-uniform
         };
-        auto make_tbl = [&](uint32_t rs, uint32_t re) {
+        auto make_tbl = [&](const Hv& rs, const Hv& re) {
             Tbl t;
-            const uint32_t n = myr_ok ? (re - rs) >> 3 : 0u;   // rs, re: 8-aligned
-            const uint32_t inc = wave_incl_scan(n);
-            t.P = inc - n;
-            t.U = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-            t.DL = ((ro + rs) >> 3) - t.P;   // unit u of the bucket is record unit u + DL
+            uint32_t tot = 0;
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                const uint32_t n = myr_ok[h] ? (re.v[h] - rs.v[h]) >> 3 : 0u;   // rs, re: 8-aligned
+                const uint32_t inc = wave_incl_scan(n) + tot;
+                t.P[h] = inc - n;
+                tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+                t.DL[h] = ((ro[h] + rs.v[h]) >> 3) - t.P[h];   // unit u of the bucket is record unit u + DL
+            }
+            t.U = tot;
             t.jn = 0;
             t.cur = 0;
             t.w0 = 0;
             return t;
         };
+        // run j's entry of a per-run table (wave-uniform j)
+        auto run_at = [&](const uint32_t (&x)[H], uint32_t j) -> uint32_t {
+            if (H == 1 || j < 64u) return (uint32_t)__builtin_amdgcn_readlane((int)x[0], (int)j);
+            return (uint32_t)__builtin_amdgcn_readlane((int)x[H - 1], (int)(j - 64u));
+        };
         constexpr int kGW = KF_BK_DB ? 4 : 8;
+        constexpr bool kPre2 = KF_BK_PRE2 && K <= 10;
         struct Grp {
             v4u v[kGW];
             uint32_t act;   // bit x: this lane's unit of window x exists
@@ -633,9 +686,9 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
                 const uint32_t w0 = t.w0 + x * kWave, u = w0 + (uint32_t)lane;
                 uint32_t dl = t.cur;
                 while (t.jn < nrun) {   // runs starting in this window
-                    const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)t.P, (int)t.jn);
+                    const uint32_t pj = run_at(t.P, t.jn);
                     if (pj >= w0 + kWave) break;
-                    const uint32_t dj = (uint32_t)__builtin_amdgcn_readlane((int)t.DL, (int)t.jn);
+                    const uint32_t dj = run_at(t.DL, t.jn);
                     dl = u >= pj ? dj : dl;
                     t.cur = dj;
                     ++t.jn;
@@ -652,12 +705,12 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             }
             t.w0 += kGW * kWave;
         };
-        auto consume = [&](const Grp& G, uint32_t U) {
+        auto consume = [&](const Grp& G, uint32_t U, uint32_t pm) {   // pm: bucket parity mask
 #pragma unroll
             for (int x = 0; x < kGW; ++x) {
                 if (G.w0 + x * kWave >= U) break;   // wave-uniform
                 if (G.act & (1u << x)) {
-                    const uint32_t d[4] = {G.v[x].x, G.v[x].y, G.v[x].z, G.v[x].w};
+                    const uint32_t d[4] = {G.v[x].x ^ pm, G.v[x].y ^ pm, G.v[x].z ^ pm, G.v[x].w ^ pm};
 #if KF_BK_ABL == 5   // profiling only: phase 2 without its histogram adds (wrong counts)
                     asm volatile("" ::"v"(d[0]), "v"(d[1]), "v"(d[2]), "v"(d[3]));
 #else
@@ -676,7 +729,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         typedef unsigned int v2u __attribute__((ext_vector_type(2)));
         auto col_at = [&](uint32_t g4) -> v2u {
             if (KF_BK_ABL == 1) {
-                const uint32_t x = (2 * g4) & 0x7FFCu;
+                const uint32_t x = (2 * g4) & (L::codes - 4u);
                 return v2u{x | (x + 1) << 16, (x + 2) | (x + 3) << 16};
             }
             return *(const v2u*)(B.col_idx + g4);
@@ -690,7 +743,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             c1 = bc[b + 1];
 #pragma unroll
             for (int x = 0; x < kFG; ++x) {
-                const uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + x * kBkBlock);
+                const uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + x * L::block);
                 const v2u c = col_at(g4 < c1 ? g4 : 0u);   // unconditional load
                 ci[x] = g4 < c1 ? c : v2u{0u, 0u};
             }
@@ -726,65 +779,84 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
             }
         };
 
-        uint32_t re_next = meta_at(1);
+        Hv re_next = meta_at(1);
         Tbl tb = make_tbl(meta_at(0), re_next);
-        uint32_t re_cur = re_next;
+        Hv re_cur = re_next;
         re_next = meta_at(NBK > 1 ? 2 : 1);
         Grp G0;
 #if KF_BK_DB
         Grp G1;
 #endif
         issue(tb, G0);
+#if KF_BK_DB
+        if constexpr (kPre2) issue(tb, G1);
+#endif
         uint64_t tp[4] = {0, 0, 0, 0};   // profile: records, barrier, flush, barrier
         uint64_t tcons = 0;              // profile: consume part of records
         for (uint32_t b = 0; b < (KF_BK_ABL == 8 ? 0u : NBK); ++b) {   // (ABL 8: phase 1 only)
             uint64_t t0 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
+            const uint32_t pm = ((b & L::hmask) << L::bits) * 0x10001u;   // both records of a word
 #if KF_BK_DB
             // two groups alternate: the bucket's next group is always in flight
             // while one is counted (issued unconditionally -- past the bucket's
             // end its lanes are inactive and read unit 0 -- so the compiler's
             // vmcnt stays exact: wait for the consumed group only)
-            for (;;) {
-                issue(tb, G1);
-                consume(G0, tb.U);
-                if (G1.w0 >= tb.U) break;
-                issue(tb, G0);
-                consume(G1, tb.U);
-                if (G0.w0 >= tb.U) break;
+            if constexpr (kPre2) {
+                // both groups were issued before the previous flush
+                for (;;) {
+                    consume(G0, tb.U, pm);
+                    if (G1.w0 >= tb.U) break;
+                    issue(tb, G0);
+                    consume(G1, tb.U, pm);
+                    if (G0.w0 >= tb.U) break;
+                    issue(tb, G1);
+                }
+            } else {
+                for (;;) {
+                    issue(tb, G1);
+                    consume(G0, tb.U, pm);
+                    if (G1.w0 >= tb.U) break;
+                    issue(tb, G0);
+                    consume(G1, tb.U, pm);
+                    if (G0.w0 >= tb.U) break;
+                }
             }
 #else
-            consume(G0, tb.U);
+            consume(G0, tb.U, pm);
             while (tb.w0 < tb.U) {   // a bucket beyond one group: synchronous groups
                 issue(tb, G0);
-                consume(G0, tb.U);
+                consume(G0, tb.U, pm);
             }
 #endif
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tcons += __builtin_amdgcn_s_memtime() - t0; }
             v2u ci[kFG];
             // issue order: bucket b+2's run ends, the flush's col_idx, bucket
             // b+1's records (vmcnt is in order: each is waited for only when used)
-            const uint32_t m = meta_at(b + 3 < NBK ? b + 3 : NBK);
+            const Hv m = meta_at(b + 3 < NBK ? b + 3 : NBK);
             uint32_t c0, c1;
             flush_issue(b, ci, c0, c1);
             if (b + 1 < NBK) {               // next bucket: table, first group in flight
                 tb = make_tbl(re_cur, re_next);   // this bucket's run ends start the next
                 re_cur = re_next;
                 issue(tb, G0);
+#if KF_BK_DB
+                if constexpr (kPre2) issue(tb, G1);
+#endif
             }
             re_next = m;
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[0] += t - t0; t0 = t; }
             lds_barrier();
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[1] += t - t0; t0 = t; }
 #pragma unroll
-            for (int x = 0; x < kFG; ++x) flush_cols((c0 & ~3u) + 4 * ((uint32_t)tid + x * kBkBlock), ci[x], c0, c1);
-            for (uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + kFG * kBkBlock); g4 < c1; g4 += 4 * kBkBlock)
+            for (int x = 0; x < kFG; ++x) flush_cols((c0 & ~3u) + 4 * ((uint32_t)tid + x * L::block), ci[x], c0, c1);
+            for (uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + kFG * L::block); g4 < c1; g4 += 4 * L::block)
                 flush_cols(g4, col_at(g4), c0, c1);
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[2] += t - t0; t0 = t; }
             lds_barrier();
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[3] += t - t0; }
         }
         if (B.prof && lane == 0) {   // per wave: records, barrier, phase-1 barrier, consume
-            unsigned long long* pw = B.prof + 8 * gridDim.x + 4 * (kBkWaves * blockIdx.x + wave);
+            unsigned long long* pw = B.prof + 8 * gridDim.x + 4 * (W * blockIdx.x + wave);
             pw[0] += tp[0];
             pw[1] += tp[1];
             pw[2] += p1w;
@@ -796,7 +868,7 @@ __global__ void __launch_bounds__(kBkBlock) bucket_kernel(CountArgs A, BucketArg
         __syncthreads();
         if (tid == 0) {
             unsigned long long t = 0;
-            for (int w = 0; w < kBkWaves; ++w) t += red[w];
+            for (int w = 0; w < W; ++w) t += red[w];
             if (t) atomicAdd(A.totals + g, t);
             if (B.prof) {
                 const uint64_t t_end = __builtin_amdgcn_s_memtime();
@@ -829,36 +901,23 @@ void* bucket_kernel_for(int k) {
     default: return nullptr;
     }
 }
-uint32_t bucket_lds_for(int k) {
+template <typename F>
+auto bucket_geom(int k, F f) {   // f(Bk<k>{}) for the compiled k
     switch (k) {
-    case 9: return Bk<9>::lds_bytes;
-    case 10: return Bk<10>::lds_bytes;
-    case 11: return Bk<11>::lds_bytes;
-    case 12: return Bk<12>::lds_bytes;
-    default: return 0;
+    case 9: return f(Bk<9>{});
+    case 10: return f(Bk<10>{});
+    case 11: return f(Bk<11>{});
+    default: return f(Bk<12>{});
     }
 }
-
-// Phase-2 rounds per wave by wave slot, packed 4 x 8 bit (slot 0 in the low byte).
-// KF_BK_WEIGHTS="a0,a1,a2,a3" (tuning/A-B knob, read per launch), each 1..32; a set
-// that could give a wave more than 64 runs of a piece is refused (default used).
-uint32_t bucket_weights() {
-    constexpr uint32_t kDefault = 0x01010101u;
-#ifndef KF_PROFILE_BUILD
-    return kDefault;   // the knob is read in profiling builds only
-#endif
-    const char* e = getenv("KF_BK_WEIGHTS");
-    if (!e || !*e) return kDefault;
-    unsigned a[4];
-    if (sscanf(e, "%u,%u,%u,%u", &a[0], &a[1], &a[2], &a[3]) != 4) return kDefault;
-    uint32_t per = 0, amax = 0;
-    for (int i = 0; i < 4; ++i) {
-        if (a[i] < 1 || a[i] > 32) return kDefault;
-        per += 4 * a[i];
-        amax = a[i] > amax ? a[i] : amax;
-    }
-    if ((kRmax / per + 1) * amax > (uint32_t)kWave) return kDefault;
-    return a[0] | a[1] << 8 | a[2] << 16 | a[3] << 24;
+uint32_t bucket_lds_for(int k) {
+    return bucket_geom(k, [](auto b) { return decltype(b)::lds_bytes; });
+}
+int bucket_waves_for(int k) {
+    return bucket_geom(k, [](auto b) { return decltype(b)::waves; });
+}
+int bucket_bits_for(int k) {
+    return bucket_geom(k, [](auto b) { return decltype(b)::bits; });
 }
 
 // Per-device state: bucket tables per k and the scratch of the last launch
@@ -871,7 +930,7 @@ struct DevState {
     uint32_t* pstart = nullptr;
     size_t pstart_n = 0;
     hipEvent_t done = nullptr;
-    int grid = 0;
+    int cus = 0;
 };
 DevState g_dev[64];
 std::mutex g_mu;
@@ -887,13 +946,15 @@ uint32_t rc_std(uint32_t s, int k) {
 
 int ensure_tables(DevState& d, int k) {
     if (d.col_idx[k]) return KF_OK;
-    const uint32_t ncode = 1u << (2 * k), nbk = ncode >> kBkBits;
+    const int bits = bucket_bits_for(k);
+    const uint32_t codes = 1u << bits;
+    const uint32_t ncode = 1u << (2 * k), nbk = ncode >> bits;
     std::vector<uint16_t> ci;
     std::vector<uint32_t> bc(nbk + 1, 0);
     ci.reserve(kf_num_bins(k));
     for (uint32_t s = 0; s < ncode; ++s) {
-        if ((s & (kBkCodes - 1)) == 0) bc[s >> kBkBits] = (uint32_t)ci.size();
-        if (s <= rc_std(s, k)) ci.push_back((uint16_t)(s & (kBkCodes - 1)));
+        if ((s & (codes - 1)) == 0) bc[s >> bits] = (uint32_t)ci.size();
+        if (s <= rc_std(s, k)) ci.push_back((uint16_t)(s & (codes - 1)));
     }
     bc[nbk] = (uint32_t)ci.size();
     if (ci.size() != kf_num_bins(k)) return kf_fail(KF_EINVAL, "bucket table: %zu canonical codes", ci.size());
@@ -915,8 +976,8 @@ int bucket_launch_info(int k, int* grid, int* block, int* lds) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return kf_fail(KF_EHIP, "device query failed");
-    *grid = cus > 0 ? cus : 1;
-    *block = kBkBlock;
+    *grid = (cus > 0 ? cus : 1) * (16 / bucket_waves_for(k));
+    *block = bucket_waves_for(k) * kWave;
     *lds = (int)bucket_lds_for(k);
     return KF_OK;
 }
@@ -932,24 +993,33 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     int rc = ensure_tables(d, k);
     if (rc) return rc;
     const uint32_t lds = bucket_lds_for(k);
-    if (!d.grid) {
+    if (!d.cus) {
         if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return kf_fail(KF_EHIP, "hipDeviceGetAttribute(MultiprocessorCount) failed");
-        d.grid = cus > 0 ? cus : 1;
+        d.cus = cus > 0 ? cus : 1;
         if (hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess)
             return kf_fail(KF_EHIP, "hipEventCreate failed");
     } else if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
         return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     }
-    const int grid = d.grid;
-    // scratch: records, round metadata (sized for the largest k), round offsets
-    const size_t nbk = ((size_t)1 << (2 * k)) >> kBkBits;
-    const size_t rec_b = (size_t)grid * ((size_t)kRmax * (kRoundRecs + 7 * nbk) + 8) * 2;   // Bk<k>::rec_cap
-    const size_t meta_b = (size_t)grid * (((1u << (2 * KF_MAX_K)) >> kBkBits) + 1) * kRmax * 2;
-    const size_t roff_b = (size_t)grid * kRmax * 4;
+    const int waves = bucket_waves_for(k);
+    const int grid = d.cus * (16 / waves);   // 16 waves per CU
+    // scratch: records, round metadata, round offsets (sized for the largest of
+    // the compiled geometries, so that a launch at another k reuses it)
+    size_t rec_b = 0, meta_b = 0, roff_b = 0;
+    for (int kk = 9; kk <= KF_MAX_K; ++kk) {   // the bucket kernels: k >= 9
+        const size_t g = (size_t)d.cus * (16 / bucket_waves_for(kk));
+        bucket_geom(kk, [&](auto b) {
+            using Lk = decltype(b);
+            rec_b = std::max(rec_b, g * (size_t)Lk::rec_cap * 2);
+            meta_b = std::max(meta_b, g * ((size_t)Lk::nbk + 1) * Lk::rmax * 2);
+            roff_b = std::max(roff_b, g * (size_t)Lk::rmax * 4);
+            return 0;
+        });
+    }
     const size_t need = rec_b + meta_b + roff_b;
     if (d.done && hipStreamWaitEvent(s, d.done, 0) != hipSuccess)
         return kf_fail(KF_EHIP, "hipStreamWaitEvent failed");
@@ -979,7 +1049,6 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     B.meta = (uint16_t*)((char*)d.scratch + rec_b);
     B.roff = (uint32_t*)((char*)d.scratch + rec_b + meta_b);
     B.accumulate = (flags & KF_ACCUMULATE) ? 1u : 0u;
-    B.slot_w = bucket_weights();
     B.prof = nullptr;
 #ifdef KF_PROFILE_BUILD
     const char* pe = getenv("KF_BUCKET_PROFILE");   // debugging aid: synchronous, prints to stderr
@@ -988,8 +1057,8 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
 #endif
     std::vector<unsigned long long> prof_h;
     if (pe && *pe == '1') {
-        if (hipMalloc((void**)&B.prof, (size_t)grid * (8 + 4 * kBkWaves) * 8) != hipSuccess ||
-            hipMemsetAsync(B.prof, 0, (size_t)grid * (8 + 4 * kBkWaves) * 8, s) != hipSuccess)
+        if (hipMalloc((void**)&B.prof, (size_t)grid * (8 + 4 * waves) * 8) != hipSuccess ||
+            hipMemsetAsync(B.prof, 0, (size_t)grid * (8 + 4 * waves) * 8, s) != hipSuccess)
             return kf_fail(KF_EHIP, "profile buffer");
     }
     hipLaunchKernelGGL(piece_scan_kernel, dim3(1), dim3(1024), 0, s, A.goff, A.n_genomes, d.pstart);
@@ -997,11 +1066,11 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
         hipLaunchKernelGGL(zero_split_rows_kernel, dim3(1024), dim3(256), 0, s, A.goff, A.n_genomes, A.counts,
                            A.nbins);
     void* args[] = {(void*)&A, (void*)&B};
-    if (hipLaunchKernel(fn, dim3(grid), dim3(kBkBlock), args, lds, s) != hipSuccess)
+    if (hipLaunchKernel(fn, dim3(grid), dim3(waves * kWave), args, lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "bucket kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (hipEventRecord(d.done, s) != hipSuccess) return kf_fail(KF_EHIP, "hipEventRecord failed");
     if (B.prof) {
-        prof_h.resize((size_t)grid * (8 + 4 * kBkWaves));
+        prof_h.resize((size_t)grid * (8 + 4 * waves));
         if (hipStreamSynchronize(s) != hipSuccess ||
             hipMemcpy(prof_h.data(), B.prof, prof_h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
             return kf_fail(KF_EHIP, "profile readback");
@@ -1010,14 +1079,18 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
         for (int i = 0; i < grid; ++i)
             for (int x = 0; x < 8; ++x) sum[x] += (double)prof_h[8 * i + x];
         const double np = sum[2] > 0 ? sum[2] : 1;
+        int occ = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)fn, waves * kWave, lds);
+        fprintf(stderr, "[kf_bucket k=%d] grid %d x %d waves, LDS %u B, resident workgroups per CU %d\n", k, grid,
+                waves, lds, occ);
         fprintf(stderr, "[kf_bucket k=%d] pieces %.0f cycles/piece: phase1 %.3g phase2 %.3g "
                 "(records %.3g, barrier %.3g, flush %.3g, barrier %.3g)\n",
                 k, sum[2], sum[0] / np, sum[1] / np, sum[3] / np, sum[4] / np, sum[5] / np, sum[6] / np);
         fprintf(stderr, "[kf_bucket k=%d] per wave, cycles per piece:", k);
-        for (int w = 0; w < kBkWaves; ++w) {
+        for (int w = 0; w < waves; ++w) {
             double v[4] = {0, 0, 0, 0};
             for (int i = 0; i < grid; ++i)
-                for (int x = 0; x < 4; ++x) v[x] += (double)prof_h[8 * grid + 4 * (kBkWaves * i + w) + x];
+                for (int x = 0; x < 4; ++x) v[x] += (double)prof_h[8 * grid + 4 * (waves * i + w) + x];
             fprintf(stderr, "\n  w%d records %.3g (consume %.3g) barrier %.3g | phase-1 barrier %.3g", w, v[0] / np,
                     v[3] / np, v[1] / np, v[2] / np);
         }

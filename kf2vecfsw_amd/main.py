@@ -183,6 +183,7 @@ def get_frequencies(args) -> None:
                 if not os.path.exists(d):
                     print("No such directory '{}'".format(d), file=sys.stderr)
                     sys.exit(0)
+            sys.stdout.flush()   # before the children write to the same stdout
             rc = _spawn_shards(_child_argv(args), world)
             if rc:
                 sys.exit(rc)
@@ -590,6 +591,10 @@ def build_parser() -> argparse.ArgumentParser:
 def main(argv=None) -> None:
     parser = build_parser()
     args = parser.parse_args(argv)
+    if os.environ.get("KF_SHARD"):
+        # a -gpus child shares its parent's stdout with the other shards: one
+        # write per line, so concurrent shards never split each other's lines
+        sys.stdout.reconfigure(line_buffering=True)
     if hasattr(args, "func"):
         args.func(args)
     else:
