@@ -61,6 +61,20 @@ namespace kf {
 #ifndef KF_NT_STORES
 #define KF_NT_STORES 1
 #endif
+// Staggered phases (see the piece loop) for k >= KF_BK_LAG (0: never): half of
+// the workgroups run one phase behind the others, with two record slots per
+// workgroup.  One process (profiles/r03/v18_lib_ab_k*_lag.json): k=10 6.55 ->
+// 6.50 ms, k=11 8.71 -> 8.46, k=12 18.67 -> 18.26; k=9 5.69 -> 5.92 (off).
+#ifndef KF_BK_LAG
+#define KF_BK_LAG 10
+#endif
+#ifndef KF_BK_LAG_SHIFT   // lagged workgroups: bit KF_BK_LAG_SHIFT of blockIdx.x (3: half of each XCD)
+#define KF_BK_LAG_SHIFT 3
+#endif
+#ifndef KF_BK_PRE2_MAXK   // KF_BK_PRE2 applies to k <= this
+#define KF_BK_PRE2_MAXK 10
+#endif
+constexpr uint32_t kBkSlots = KF_BK_LAG ? 2u : 1u;   // record / meta / roff slots per workgroup
 
 // Workgroup shape (per k, compile time): W = 16 waves, one workgroup per CU,
 // 32768-code buckets (a 128 KiB histogram); or W = 8 waves, two workgroups per
@@ -346,25 +360,52 @@ bucket_kernel(CountArgs A, BucketArgs B) {
     for (uint32_t i = tid; i < L::codes + NBK; i += L::block) lds[i] = 0;   // histogram + counters
     __syncthreads();
 
-    uint16_t* rec = B.rec + (uint64_t)blockIdx.x * L::rec_cap;
-    uint16_t* meta = B.meta + (uint64_t)blockIdx.x * (NBK + 1) * L::rmax;
-    uint32_t* roff = B.roff + (uint64_t)blockIdx.x * L::rmax;
     const uint32_t npiece = B.pstart[A.n_genomes];
-
-    for (uint32_t p = blockIdx.x; p < npiece; p += gridDim.x) {
+    // This workgroup's pieces are blockIdx.x + i gridDim.x (i < nmine).  With
+    // lag = 1 it runs phase 1 of piece i before phase 2 of piece i - 1 (two record
+    // slots), so that half of the CUs (every other group of 8 workgroups: half of
+    // each XCD) are in the LDS-bound phase 1 while the others stream phase 2's
+    // records and rows, instead of all CUs switching phase together.
+    constexpr bool kLagK = KF_BK_LAG && K >= KF_BK_LAG;
+    const uint32_t lag = kLagK ? ((blockIdx.x >> KF_BK_LAG_SHIFT) & 1u) : 0u;
+    const uint32_t nmine = blockIdx.x < npiece ? (npiece - 1u - blockIdx.x) / gridDim.x + 1u : 0u;
+    struct Piece {
+        int32_t g;
+        uint32_t np, pi, nround;
+        uint64_t glo, ghi, plo, phi;
+    };
+    auto piece_at = [&](uint32_t p) -> Piece {
+        Piece P;
         // genome of piece p: last g with pstart[g] <= p
-        const int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, p, lane,
-                                                    [&](uint64_t i) { return (uint64_t)B.pstart[i]; }) - 1;
-        const uint32_t np = B.pstart[g + 1] - B.pstart[g], pi = p - B.pstart[g];
-        const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
-        const uint64_t plo = split_at(glo, ghi, pi, np), phi = split_at(glo, ghi, pi + 1, np);
-        const uint64_t lo = split_at(plo, phi, wave, W), hi = split_at(plo, phi, wave + 1, W);
+        P.g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, p, lane,
+                                        [&](uint64_t i) { return (uint64_t)B.pstart[i]; }) - 1;
+        P.np = B.pstart[P.g + 1] - B.pstart[P.g];
+        P.pi = p - B.pstart[P.g];
+        P.glo = A.goff[P.g];
+        P.ghi = A.goff[P.g + 1];
+        P.plo = split_at(P.glo, P.ghi, P.pi, P.np);
+        P.phi = split_at(P.glo, P.ghi, P.pi + 1, P.np);
         // rounds = the longest wave range in chunks (same value in every wave)
-        uint32_t nround = 0;
+        P.nround = 0;
         for (int w = 0; w < W; ++w) {
-            const uint64_t a = split_at(plo, phi, w, W), e = split_at(plo, phi, w + 1, W);
-            if (e > a) nround = max(nround, (uint32_t)((e - (a & ~(uint64_t)15) + kChunk - 1) / kChunk));
+            const uint64_t a = split_at(P.plo, P.phi, w, W), e = split_at(P.plo, P.phi, w + 1, W);
+            if (e > a) P.nround = max(P.nround, (uint32_t)((e - (a & ~(uint64_t)15) + kChunk - 1) / kChunk));
         }
+        return P;
+    };
+
+    for (uint32_t it = 0; it < nmine + lag; ++it) {
+      if (it < nmine) {
+        const uint32_t slot = kLagK ? (it & 1u) : 0u;
+        uint16_t* rec = B.rec + ((uint64_t)blockIdx.x * kBkSlots + slot) * L::rec_cap;
+        uint16_t* meta = B.meta + ((uint64_t)blockIdx.x * kBkSlots + slot) * (NBK + 1) * L::rmax;
+        uint32_t* roff = B.roff + ((uint64_t)blockIdx.x * kBkSlots + slot) * L::rmax;
+        const Piece P = piece_at(blockIdx.x + it * gridDim.x);
+        const int32_t g = P.g;
+        const uint64_t glo = P.glo, ghi = P.ghi, plo = P.plo, phi = P.phi;
+        const uint32_t nround = P.nround;
+        const uint64_t lo = split_at(plo, phi, wave, W), hi = split_at(plo, phi, wave + 1, W);
+        (void)g;
 
         // ---------------------------------------------------------- phase 1
         const uint64_t t_p1 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -600,6 +641,17 @@ bucket_kernel(CountArgs A, BucketArgs B) {
         if (r < nround) round(r++, buf[2]);
         lds_barrier();
         if (nround > 0) copy_out(nround - 1, t_prev, off_prev);
+        if (B.prof && tid == 0) B.prof[8 * blockIdx.x] += __builtin_amdgcn_s_memtime() - t_p1;
+        if (B.prof && lane == 0) B.prof[8 * gridDim.x + 4 * (W * blockIdx.x + wave) + 2] += p1w;
+      }
+      if (it >= lag) {
+        const uint32_t slot = kLagK ? ((it - lag) & 1u) : 0u;
+        uint16_t* rec = B.rec + ((uint64_t)blockIdx.x * kBkSlots + slot) * L::rec_cap;
+        uint16_t* meta = B.meta + ((uint64_t)blockIdx.x * kBkSlots + slot) * (NBK + 1) * L::rmax;
+        uint32_t* roff = B.roff + ((uint64_t)blockIdx.x * kBkSlots + slot) * L::rmax;
+        const Piece P = piece_at(blockIdx.x + (it - lag) * gridDim.x);
+        const int32_t g = P.g;
+        const uint32_t np = P.np, nround = P.nround;
 
         // ---------------------------------------------------------- phase 2
         // records and meta were stored by other waves of this workgroup: wait for
@@ -671,7 +723,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             return (uint32_t)__builtin_amdgcn_readlane((int)x[H - 1], (int)(j - 64u));
         };
         constexpr int kGW = KF_BK_DB ? 4 : 8;
-        constexpr bool kPre2 = KF_BK_PRE2 && K <= 10;
+        constexpr bool kPre2 = KF_BK_PRE2 && K <= KF_BK_PRE2_MAXK;
         struct Grp {
             v4u v[kGW];
             uint32_t act;   // bit x: this lane's unit of window x exists
@@ -855,11 +907,10 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             lds_barrier();
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[3] += t - t0; }
         }
-        if (B.prof && lane == 0) {   // per wave: records, barrier, phase-1 barrier, consume
+        if (B.prof && lane == 0) {   // per wave: records, barrier, (phase-1 barrier), consume
             unsigned long long* pw = B.prof + 8 * gridDim.x + 4 * (W * blockIdx.x + wave);
             pw[0] += tp[0];
             pw[1] += tp[1];
-            pw[2] += p1w;
             pw[3] += tcons;
         }
         tsum = wave_sum(tsum);
@@ -872,13 +923,13 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             if (t) atomicAdd(A.totals + g, t);
             if (B.prof) {
                 const uint64_t t_end = __builtin_amdgcn_s_memtime();
-                B.prof[8 * blockIdx.x] += t_p2 - t_p1;
                 B.prof[8 * blockIdx.x + 1] += t_end - t_p2;
                 B.prof[8 * blockIdx.x + 2] += 1;
                 for (int x = 0; x < 4; ++x) B.prof[8 * blockIdx.x + 3 + x] += tp[x];
             }
         }
         __syncthreads();
+      }
     }
 }
 
@@ -1011,7 +1062,7 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     // the compiled geometries, so that a launch at another k reuses it)
     size_t rec_b = 0, meta_b = 0, roff_b = 0;
     for (int kk = 9; kk <= KF_MAX_K; ++kk) {   // the bucket kernels: k >= 9
-        const size_t g = (size_t)d.cus * (16 / bucket_waves_for(kk));
+        const size_t g = (size_t)d.cus * (16 / bucket_waves_for(kk)) * kBkSlots;
         bucket_geom(kk, [&](auto b) {
             using Lk = decltype(b);
             rec_b = std::max(rec_b, g * (size_t)Lk::rec_cap * 2);

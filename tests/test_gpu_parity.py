@@ -346,6 +346,26 @@ def test_bucket_kernel_synth_batch_vs_oracle(torch_dev, oracle, k):
     assert int(totals.sum()) == int(counts.astype(np.uint64).sum())
 
 
+@pytest.mark.parametrize("k", [9, 10, 11])
+def test_bucket_staggered_pieces_every_genome(torch_dev, oracle, k):
+    """Several pieces per workgroup (1,100 genomes on a 256-workgroup grid), so
+    that the staggered workgroups (phase 1 of piece i before phase 2 of piece
+    i - 1, two record slots) alternate slots and the others do not: every
+    genome bit-exact vs the oracle."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    n = 1100
+    db = C.synth_device_batch(n, 24_000, seed0=77, n_period=5, device=torch_dev)
+    cnt, tot = counter(k, torch_dev).count(db)
+    torch.cuda.synchronize()
+    totals = tot.cpu().numpy()
+    host = db.data.cpu().numpy()
+    off = db.off.cpu().numpy()
+    for i in range(n):   # row by row (k = 11: 8 MiB per row)
+        c, t = oracle.count(host[off[i]: off[i + 1]].tobytes(), k)
+        assert int(totals[i]) == t and (C.counts_to_numpy(cnt[i]) == c).all(), i
+
+
 @pytest.mark.parametrize("k", [3, 5, 6, 7, 8])
 def test_ragged_fasta_medium_genomes(torch_dev, oracle, k):
     """K1 (k <= 6) and K1x (k = 7, 8) on ragged multi-record FASTA of up to
