@@ -13,7 +13,7 @@ tail -1 "$OUT/smoke.log"
 timeout -k 10 400 python bench.py > "$OUT/bench.log" 2>&1 || { echo "bench rc=$?"; tail -5 "$OUT/bench.log"; exit 1; }
 tail -1 "$OUT/bench.log" | cut -c1-400
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -f csv -- python3 "$REPO/bench.py" --steps 10 --warmup 2 --no-cpu --verify 0 > "$OUT/prof.log" 2>&1 || { echo "rocprof rc=$?"; tail -5 "$OUT/prof.log"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -f csv -- python3 "$REPO/bench.py" --steps 50 --warmup 10 --no-cpu --verify 0 > "$OUT/prof.log" 2>&1 || { echo "rocprof rc=$?"; tail -5 "$OUT/prof.log"; exit 1; }
 tail -1 "$OUT/prof.log" | cut -c1-300
 cd "$REPO"
 K_LIST="${TRAFFIC_K:-7 11}" ROUND=r03 bash tools/traffic_round.sh || exit $?
