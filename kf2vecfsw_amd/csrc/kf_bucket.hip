@@ -75,6 +75,18 @@ namespace kf {
 #define KF_BK_PRE2_MAXK 10
 #endif
 constexpr uint32_t kBkSlots = KF_BK_LAG ? 2u : 1u;   // record / meta / roff slots per workgroup
+// Wave priority by age slot (tools/ A/B builds): bit 0 = phase 1, bit 1 = phase 2
+// run at s_setprio(wave >> 2), so that the youngest wave of each SIMD (which the
+// SIMD issues last) is not the one every barrier waits for.
+#ifndef KF_BK_PRIO
+#define KF_BK_PRIO 0
+#endif
+__device__ __forceinline__ void bk_setprio(uint32_t p) {   // p wave-uniform
+    if (p == 0) __builtin_amdgcn_s_setprio(0);
+    else if (p == 1) __builtin_amdgcn_s_setprio(1);
+    else if (p == 2) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+}
 
 // Workgroup shape (per k, compile time): W = 16 waves, one workgroup per CU,
 // 32768-code buckets (a 128 KiB histogram); or W = 8 waves, two workgroups per
@@ -409,6 +421,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
 
         // ---------------------------------------------------------- phase 1
         const uint64_t t_p1 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
+        if (KF_BK_PRIO) bk_setprio((KF_BK_PRIO & 1) ? (uint32_t)wave >> 2 : 0u);
         Range rg;
         uint32_t nch = 0;
         if (lo < hi) {
@@ -657,6 +670,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
         // records and meta were stored by other waves of this workgroup: wait for
         // the stores, and read them with L1-bypassing loads below
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (KF_BK_PRIO) bk_setprio((KF_BK_PRIO & 2) ? (uint32_t)wave >> 2 : 0u);
         const uint64_t t_p2 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
         for (uint32_t i = tid; i < L::dirty / 4; i += L::block) lds_st(L::hist + 4 * i, 0u);   // phase-1 area
         lds_barrier();
