@@ -96,9 +96,10 @@ int kf_index_records(const uint8_t* bytes, uint64_t len, int fmt, uint64_t base,
  *   d_counts   : n_genomes x nbins uint32 (column order), zeroed first unless
  *                flags & KF_ACCUMULATE
  *   d_totals   : n_genomes uint64, number of k-mers counted per genome
- * Asynchronous on `stream`.  For k >= 10 the library counts through a device
- * workspace it allocates on first use (about 4.5 GB on a 256-CU device: 2 bytes
- * of sorted records per byte of the 8 MiB genome piece each CU holds) and keeps
+ * Asynchronous on `stream`.  For k >= 9 the library counts through a device
+ * workspace it allocates on first use (about 9 GB on a 256-CU device: 2 bytes
+ * of sorted records per byte of the 8 MiB genome piece each CU holds, in two
+ * slots for the staggered phases) and keeps
  * until kf_workspace_release(); launches on different streams of one device
  * that use it are ordered by the library. */
 int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
