@@ -24,10 +24,16 @@ launch (rocprofv3 PMC, tools/pmc_traffic.py) when profiles/ holds it.
 `roofline.achieved` = algorithmic bytes per launch (FASTA bytes read + 4 B x
 bins written) / the count kernel's average duration,
 timed with HIP events on the launch stream inside the timed region.
+`roofline.cold_kernel_ms` is one launch after the GPU has idled for a second
+(what a CLI batch that follows host I/O sees), measured after the timed region.
 The CPU baseline (rank 0, N=1) times the oracle's C restatement (kind "port":
 Jellyfish is not installed) on a bounded sample of the same genomes, OpenMP
 over (genome, ~1 MiB part) pairs on every host CPU this process may use
 (sched_getaffinity, capped by a cgroup CPU quota if one is set).
+`e2e` (rank 0, N=1) is the get_frequencies CLI end to end on 64 bacterial-like
+~5 Mbp genome files in tmpfs (BASELINE configs[2] shape): the pipelined CLI
+wall time, and the same work run stage by stage (read + record index, H2D,
+count, D2H, format + write) to show where the time goes.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--k 7]
   (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
@@ -49,9 +55,34 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 SEED = 20260101
 
-
 CONFIG3_GENOMES = 50_000          # BASELINE.json configs[3]
 SUB_BATCH = 6_250                 # genomes per resident sub-batch (the N=8 shard)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--k", type=int, default=7)
+    ap.add_argument("--workload", choices=["auto", "configs1", "configs3"], default="auto",
+                    help="auto: configs1 (1,000 genomes per GPU) at N=1, configs3 (50,000 genomes sharded) at N>1")
+    ap.add_argument("--genomes-per-gpu", type=int, default=1000, help="configs1 batch per GPU")
+    ap.add_argument("--total-genomes", type=int, default=CONFIG3_GENOMES, help="configs3 batch over all GPUs")
+    ap.add_argument("--sub-batch", type=int, default=SUB_BATCH, help="configs3 genomes per resident sub-batch")
+    ap.add_argument("--max-resident-gb", type=float, default=0.0,
+                    help="configs3: HBM budget per rank for resident sub-batches (0 = free memory - 8 GB)")
+    ap.add_argument("--seq-len", type=int, default=5_000_000)
+    ap.add_argument("--cpu-sample-genomes", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable host CPU")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--secondary-k", type=int, default=11,
+                    help="also time this k on the same batch (BASELINE configs[4]); 0 = off; N=1 only")
+    ap.add_argument("--verify", type=int, default=4, help="genomes per rank checked bit-exactly against the oracle")
+    ap.add_argument("--e2e-genomes", type=int, default=64, help="CLI end-to-end files (0 = off; N=1 only)")
+    ap.add_argument("--e2e-len", type=int, default=5_000_000)
+    return ap.parse_args(argv)
 
 
 def shard_ids(n_per_rank: int, rank: int, world: int) -> tuple[int, int]:
@@ -96,10 +127,15 @@ def usable_cpus() -> tuple[int, dict]:
     return n, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(args, ids: list[int]) -> dict:
-    """Oracle C restatement on host cores over a bounded sample (~10 s of CPU work)."""
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import kf_oracle as O
+    return O
+
+
+def cpu_baseline(args, ids: list[int]) -> dict:
+    """Oracle C restatement on host cores over a bounded sample (~10 s of CPU work)."""
+    O = _oracle()
     O.build()
     usable, cpu_info = usable_cpus()
     threads = int(args.cpu_threads) if args.cpu_threads else usable
@@ -134,7 +170,7 @@ def cpu_baseline(args, ids: list[int]) -> dict:
                       f"on {threads} threads, k={args.k})"}
 
 
-def stream_ceiling(torch, data, stream) -> dict:
+def stream_ceiling(torch, data, stream, reps: int = 5) -> dict:
     """Practical HBM read ceilings on this device, measured on the resident batch
     (SURVEY section 8(d) asks for a measured ceiling beside the spec peak):
     the count kernel's own access pattern with no counting (kf_stream_probe)
@@ -158,11 +194,11 @@ def stream_ceiling(torch, data, stream) -> dict:
     def probe():
         N.check(N.lib().kf_stream_probe(data.data_ptr(), n, out.data_ptr(), stream.cuda_stream), "kf_stream_probe")
 
-    t_probe = timed(probe)
-    t_copy = timed(lambda: dst.copy_(data[:n]))
+    t_probe = timed(probe, reps)
+    t_copy = timed(lambda: dst.copy_(data[:n]), 5)
     del dst
     return {"stream_read_GBps": round(n / t_probe / 1e9, 1), "d2d_copy_GBps": round(2 * n / t_copy / 1e9, 1),
-            "bytes": int(n)}
+            "bytes": int(n), "probe_reps": reps + 1, "copy_reps": 6}
 
 
 def load_traffic(k: int, workload_tag: str):
@@ -179,28 +215,294 @@ def load_traffic(k: int, workload_tag: str):
     return None, None
 
 
+class Workload:
+    """One rank's share of the bench workload: configs[1] (one batch of
+    --genomes-per-gpu) or configs[3] (the rank's round-robin shard of
+    --total-genomes in sub-batches), generated on the device, counted, checked."""
+
+    def __init__(self, args, dev, rank: int = 0, world: int = 1, dist=None, rehearse: bool = False):
+        import torch
+        from kf2vecfsw_amd import counter as C
+        self.args, self.dev, self.rank, self.world, self.dist, self.rehearse = args, dev, rank, world, dist, rehearse
+        self.torch, self.C = torch, C
+        self.kind = args.workload if args.workload != "auto" else ("configs1" if world == 1 else "configs3")
+        if self.kind == "configs1":
+            g0, gs = shard_ids(args.genomes_per_gpu, rank, world)
+            self.plan = [(g0, gs, args.genomes_per_gpu)]
+        else:
+            self.plan = shard_plan(args.total_genomes, rank, world, args.sub_batch)
+        self.n = sum(c for _, _, c in self.plan)                      # this rank's genomes
+        self.nsb = sum(1 for _, _, c in self.plan if c)
+        self.sb_bytes = [int(C.synth_layout(c, args.seq_len, 80, a, st)[-1]) if c else 0 for a, st, c in self.plan]
+        self.fasta_bytes = sum(C.synth_fasta_bytes(args.seq_len, 80, a + i * st)
+                               for a, st, c in self.plan for i in range(c))
+        self.stream = torch.cuda.current_stream(dev)
+
+    # ---- collectives (RCCL / gloo: barriers and max-over-ranks only)
+    def _tensor(self, v, dtype=None):
+        return self.torch.tensor(v, dtype=dtype, device=self.dev if not self.rehearse else "cpu")
+
+    def barrier(self):
+        if self.world > 1 and self.dist is not None:
+            self.dist.barrier()
+
+    def all_ok(self, ok: bool) -> bool:
+        if self.world > 1 and self.dist is not None:
+            f = self._tensor([0.0 if ok else 1.0])
+            self.dist.all_reduce(f, op=self.dist.ReduceOp.MAX)
+            ok = float(f) == 0.0
+        return ok
+
+    def max_over_ranks(self, *v):
+        if self.world == 1 or self.dist is None:
+            return v
+        t = self._tensor(v, self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return tuple(float(x) for x in t)
+
+    def fits(self, kmax: int) -> bool:
+        """Whether every sub-batch (and its count rows at kmax) stays resident."""
+        row_b = 4 * self.C.num_bins(kmax) + 8
+        need = sum(self.sb_bytes) + row_b * self.n
+        a = self.args
+        budget = a.max_resident_gb * 1e9 if a.max_resident_gb else self.torch.cuda.mem_get_info(self.dev)[0] - 8e9
+        resident = need <= budget
+        if self.world > 1:   # every rank takes the same mode (the streamed mode has per-sub-batch barriers)
+            resident = self.all_ok(resident)
+        return resident
+
+    # ---- device batches and timed passes
+    def gen(self, j):
+        a, st, c = self.plan[j]
+        if not c:
+            return None
+        db = self.C.synth_device_batch(c, self.args.seq_len, SEED, width=80, g0=a, g_stride=st, device=self.dev)
+        self.torch.cuda.synchronize(self.dev)
+        return db
+
+    def run(self, k, steps, warmup, dbs, pre=None):
+        """`warmup` untimed + `steps` timed steps at k over the sub-batches `dbs`
+        (None = empty).  A step = one kf_count_batch call (count-matrix memset +
+        kernel) per sub-batch.  `pre(dbs)` runs before the warmup steps.  Returns
+        (counter, outputs, wall s, HIP-event ms of every timed launch on the launch
+        stream, HIP-event ms of the warmup launches)."""
+        torch, stream = self.torch, self.stream
+        kc = self.C.KmerCounter(k, self.dev)
+        kc.reserve(max((db.n for db in dbs if db is not None), default=0))
+        outs = [kc.alloc_out(db.n) if db is not None else None for db in dbs]
+        if pre is not None:
+            pre(dbs)
+
+        def step(evs=None):
+            for db, o in zip(dbs, outs):
+                if db is None:
+                    continue
+                if evs is not None:
+                    e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    e[0].record(stream)
+                kc.count(db, o[0], o[1], accumulate=False)   # the CLI's call
+                if evs is not None:
+                    e[1].record(stream)
+                    evs.append(e)
+
+        wevs = []
+        for _ in range(warmup):
+            step(wevs)
+        torch.cuda.synchronize(self.dev)
+        evs = []
+        self.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(evs)
+        torch.cuda.synchronize(self.dev)
+        self.barrier()
+        el = time.perf_counter() - t0
+        return kc, outs, el, [a.elapsed_time(b) for a, b in evs], [a.elapsed_time(b) for a, b in wevs]
+
+    def verify(self, k, j, outs, picks) -> bool:
+        """Totals are analytic for N-free synthetic genomes; `picks` genomes of
+        sub-batch j (evenly spaced, first and last included; all if picks >= its
+        size) bit-exact vs the oracle -- the checker, outside the timed region."""
+        a, st, c = self.plan[j]
+        ok = True
+        for o in outs:
+            if o is None:
+                continue
+            ok &= bool((o[1].cpu().numpy() == self.args.seq_len - k + 1).all())
+        if picks and c and outs and outs[0] is not None:
+            O = _oracle()
+            cnp = self.C.counts_to_numpy(outs[0][0])
+            for i in np.unique(np.linspace(0, c - 1, min(picks, c)).astype(int)):
+                g = a + int(i) * st
+                cc, t = O.count(O.synth_genome(g, SEED + g, self.args.seq_len, 80), k)
+                ok &= bool((cnp[i] == cc).all()) and int(outs[0][1][i]) == t
+        return ok
+
+    def measure(self, k, steps, warmup, resident, picks, picks_rest=0, keep=False, pre=None):
+        """The timed passes at k over this rank's plan: resident (every sub-batch in
+        HBM, one step = all of them) or streamed (each sub-batch generated, timed on
+        its own, the times added).  `picks` genomes of the first sub-batch and
+        `picks_rest` of every other one are checked against the oracle; `pre` (see
+        run) before the first timed pass.  Returns a dict with the wall time,
+        per-launch ms, the parity verdict of this rank, and (keep=True, resident)
+        the batches."""
+        res = {"ok": True, "launch_ms": [], "warm_ms": [], "el": 0.0, "dbs": None, "kc": None, "outs": None}
+        if resident:
+            dbs = [self.gen(j) for j in range(len(self.plan))]
+            kc, outs, el, ms, wms = self.run(k, steps, warmup, dbs, pre)
+            for j in range(len(self.plan)):
+                res["ok"] &= self.verify(k, j, [outs[j]], picks if j == 0 else picks_rest)
+            res.update(el=el, launch_ms=ms, warm_ms=wms, kc=kc, dbs=dbs if keep else None,
+                       outs=outs if keep else None)
+            del outs
+        else:
+            for j in range(len(self.plan)):
+                db = self.gen(j)
+                kc, outs, e, ms, wms = self.run(k, steps, warmup, [db], pre if j == 0 else None)
+                res["el"] += e
+                res["launch_ms"] += ms
+                res["warm_ms"] += wms
+                res["ok"] &= self.verify(k, j, outs, picks if j == 0 else picks_rest)
+                res["kc"] = kc
+                del outs, db
+        return res
+
+
+def cold_launch_ms(torch, kc, db, stream, idle_s: float = 1.0) -> float:
+    """One launch after the GPU has idled `idle_s` (what a CLI batch sees after host I/O)."""
+    out = kc.alloc_out(db.n)
+    torch.cuda.synchronize()
+    time.sleep(idle_s)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    kc.count(db, out[0], out[1])
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b)
+
+
+# ---------------------------------------------------------------------------
+# e2e: the get_frequencies CLI on real-shaped files (BASELINE configs[2] shape)
+# ---------------------------------------------------------------------------
+def bacterial_like(rng: np.random.Generator, total: int) -> tuple[bytes, int]:
+    """A synthetic bacterial-like assembly (no assemblies offline): 1-80 contigs,
+    GC 30-70 %, short N runs, 60/80-column lines, soft-masked stretches.
+    Returns the FASTA bytes and its number of sequence characters."""
+    ncontig = int(rng.integers(1, 81))
+    cuts = np.sort(rng.choice(np.arange(1, total), size=ncontig - 1, replace=False)) if ncontig > 1 else []
+    lens = np.diff(np.concatenate([[0], cuts, [total]])).astype(np.int64)
+    gc = float(rng.uniform(0.3, 0.7))
+    width = int(rng.choice([60, 80]))
+    lut = np.frombuffer(b"ACGT", np.uint8)
+    p = np.array([(1 - gc) / 2, gc / 2, gc / 2, (1 - gc) / 2])
+    out = []
+    for i, L in enumerate(lens):
+        seq = lut[rng.choice(4, size=int(L), p=p)]
+        for _ in range(int(rng.poisson(L * 1e-6)) + 0):
+            a = int(rng.integers(0, L))
+            seq[a: a + int(rng.integers(1, 40))] = ord("N")
+        if rng.random() < 0.3 and L > 2000:
+            a = int(rng.integers(0, L - 1000))
+            seq[a: a + 1000] |= 0x20
+        nl = (int(L) + width - 1) // width
+        body = np.full(int(L) + nl, 10, np.uint8)
+        idx = np.arange(int(L))
+        body[idx + idx // width] = seq
+        out.append(b">contig_%d len=%d\n" % (i, L) + body.tobytes())
+    return b"".join(out), int(total)
+
+
+def e2e_bench(args, dev) -> dict:
+    """The get_frequencies CLI (kf2vecfsw_amd.main) on --e2e-genomes files in
+    tmpfs, k=7: median pipelined wall time of 3 runs after a warm run; then the
+    same files stage by stage with a sync between stages.  Four .kf files are
+    checked against the oracle (outside the timing)."""
+    import contextlib
+    import io
+    import tempfile
+
+    import torch
+    from kf2vecfsw_amd import counter as C
+    from kf2vecfsw_amd import main as M
+    threads, _ = usable_cpus()
+    base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else None
+    work = tempfile.mkdtemp(prefix="kf_e2e_", dir=base)
+    try:
+        inp = os.path.join(work, "in")
+        os.makedirs(inp)
+        rng = np.random.default_rng(2026)
+        bases = 0
+        names = []
+        for g in range(args.e2e_genomes):
+            blob, nb = bacterial_like(rng, args.e2e_len)
+            bases += nb
+            names.append("B%04d" % g)
+            with open(os.path.join(inp, names[-1] + ".fna"), "wb") as f:
+                f.write(blob)
+        in_bytes = sum(os.path.getsize(os.path.join(inp, n + ".fna")) for n in names)
+
+        def cli(out):
+            os.makedirs(out)
+            with contextlib.redirect_stdout(io.StringIO()):
+                t0 = time.perf_counter()
+                M.main(["get_frequencies", "-input_dir", inp, "-output_dir", out, "-k", str(7), "-p", str(threads)])
+                return time.perf_counter() - t0
+
+        walls = [cli(os.path.join(work, f"out{r}")) for r in range(4)]
+        wall = float(np.median(walls[1:]))
+        # stage by stage (one batch of every file, synchronised between stages)
+        files = sorted(os.listdir(inp))
+        paths = [os.path.join(inp, f) for f in files]
+        kc = C.KmerCounter(7, dev)
+        stream = torch.cuda.current_stream(dev)
+        st = {}
+        for rep in range(2):   # the first pass warms the pinned allocator
+            t0 = time.perf_counter()
+            hb = C.pack_files(paths, [f.rsplit(".f", 1)[0] for f in files], threads=threads)
+            t1 = time.perf_counter()
+            db = C.to_device(hb, dev)
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+            cnt, _ = kc.count(db)
+            torch.cuda.synchronize(dev)
+            t3 = time.perf_counter()
+            host = torch.empty(cnt.shape, dtype=cnt.dtype, pin_memory=True)
+            host.copy_(cnt, non_blocking=True)
+            stream.synchronize()
+            t4 = time.perf_counter()
+            outd = os.path.join(work, f"stage{rep}")
+            os.makedirs(outd)
+            M.write_kf_files(outd, hb.names, host.numpy().view(np.uint32), False, False, threads)
+            t5 = time.perf_counter()
+            st = {"read_index": t1 - t0, "h2d": t2 - t1, "count": t3 - t2, "d2h": t4 - t3, "format_write": t5 - t4}
+            del hb, db, cnt, host
+        O = _oracle()
+        ok = True
+        for g in np.linspace(0, len(names) - 1, 4).astype(int):
+            data = open(os.path.join(inp, names[g] + ".fna"), "rb").read()
+            c, _ = O.count(data, 7)
+            exp = O.kf_line(names[g], c).encode()
+            ok &= open(os.path.join(work, "out1", names[g] + ".kf"), "rb").read() == exp
+            ok &= open(os.path.join(work, "stage1", names[g] + ".kf"), "rb").read() == exp
+        out_bytes = sum(os.path.getsize(os.path.join(work, "out1", n + ".kf")) for n in names)
+        gbs = lambda s: round(bases / s / 1e9, 3)
+        return {"workload": f"get_frequencies CLI, k=7, {len(names)} bacterial-like ~{args.e2e_len / 1e6:g} Mbp "
+                            f"FASTA files in {'/dev/shm' if base else 'tmp'} (BASELINE configs[2] shape)",
+                "bases": bases, "input_bytes": in_bytes, "kf_bytes": out_bytes, "host_threads": threads,
+                "cli_wall_s": round(wall, 4), "cli_wall_s_runs": [round(w, 4) for w in walls],
+                "value": gbs(wall), "unit": "Gbases/s",
+                "stages_s": {k: round(v, 4) for k, v in st.items()},
+                "stages_Gbases_s": {k: gbs(v) for k, v in st.items()},
+                "stages_sum_s": round(sum(st.values()), 4),
+                "pcie_h2d_GBps": round(in_bytes / st["h2d"] / 1e9, 1) if st.get("h2d") else None,
+                "parity": "ok" if ok else "MISMATCH"}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
 def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--k", type=int, default=7)
-    ap.add_argument("--workload", choices=["auto", "configs1", "configs3"], default="auto",
-                    help="auto: configs1 (1,000 genomes per GPU) at N=1, configs3 (50,000 genomes sharded) at N>1")
-    ap.add_argument("--genomes-per-gpu", type=int, default=1000, help="configs1 batch per GPU")
-    ap.add_argument("--total-genomes", type=int, default=CONFIG3_GENOMES, help="configs3 batch over all GPUs")
-    ap.add_argument("--sub-batch", type=int, default=SUB_BATCH, help="configs3 genomes per resident sub-batch")
-    ap.add_argument("--max-resident-gb", type=float, default=0.0,
-                    help="configs3: HBM budget per rank for resident sub-batches (0 = free memory - 8 GB)")
-    ap.add_argument("--seq-len", type=int, default=5_000_000)
-    ap.add_argument("--cpu-sample-genomes", type=int, default=64)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable host CPU")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--secondary-k", type=int, default=11,
-                    help="also time this k on the same batch (BASELINE configs[4]); 0 = off; N=1 only")
-    ap.add_argument("--verify", type=int, default=4, help="genomes per rank checked bit-exactly against the oracle")
-    args = ap.parse_args()
+    args = parse_args()
 
     import torch
     import torch.distributed as dist
@@ -225,143 +527,47 @@ def main() -> None:
 
     from kf2vecfsw_amd import build as B
     B.build()
-    from kf2vecfsw_amd import counter as C
+    from kf2vecfsw_amd import _native as N
 
-    workload = args.workload if args.workload != "auto" else ("configs1" if world == 1 else "configs3")
-    if workload == "configs1":
-        g0, gs = shard_ids(args.genomes_per_gpu, rank, world)
-        plan = [(g0, gs, args.genomes_per_gpu)]
-    else:
-        plan = shard_plan(args.total_genomes, rank, world, args.sub_batch)
-    n = sum(c for _, _, c in plan)                                  # this rank's genomes
-    sb_bytes = [int(C.synth_layout(c, args.seq_len, 80, a, st)[-1]) if c else 0 for a, st, c in plan]
+    W = Workload(args, dev, rank, world, dist if world > 1 else None, rehearse)
     kmax = max(args.k, args.secondary_k if (world == 1 and args.secondary_k) else 0)
-    row_b = 4 * C.num_bins(kmax) + 8
-    need = sum(sb_bytes) + row_b * n
-    budget = args.max_resident_gb * 1e9 if args.max_resident_gb else torch.cuda.mem_get_info(dev)[0] - 8e9
-    resident = need <= budget
-    if world > 1:   # every rank takes the same mode (the streamed mode has per-sub-batch barriers)
-        f = torch.tensor([0.0 if resident else 1.0], device=dev if not rehearse else "cpu")
-        dist.all_reduce(f, op=dist.ReduceOp.MAX)
-        resident = float(f) == 0.0
-    stream = torch.cuda.current_stream(dev)
-    bases = n * args.seq_len
-    fasta_bytes = sum(C.synth_fasta_bytes(args.seq_len, 80, a + i * st) for a, st, c in plan for i in range(c))
+    resident = W.fits(kmax)
+    stream = W.stream
+    bases = W.n * args.seq_len
 
-    def gen(j):
-        a, st, c = plan[j]
-        if not c:
-            return None
-        db = C.synth_device_batch(c, args.seq_len, SEED, width=80, g0=a, g_stride=st, device=dev)
-        torch.cuda.synchronize(dev)
-        return db
+    # The measured-ceiling probes run on the generated batch BEFORE the warmup
+    # steps: they stream it ~60 times (about 70 ms of HBM traffic), after which
+    # the GPU's clocks have settled; right after generation or an idle gap the
+    # first ~20 count launches run up to 40 % slower while they settle
+    # (profiles/r04/v1_cold.json).  Declared in the JSON ("prewarm"); the launch
+    # after an idle second is reported as roofline.cold_kernel_ms.
+    ceiling = {}
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
+    def prewarm(dbs):
+        db0 = next((d for d in dbs if d is not None), None)
+        if db0 is not None:
+            ceiling.update(stream_ceiling(torch, db0.data, stream, reps=60))
 
-    def run(k, steps, warmup, dbs):
-        """`warmup` untimed + `steps` timed steps at k over the sub-batches `dbs`
-        (None = empty).  A step = one kf_count_batch call (count-matrix memset +
-        kernel) per sub-batch.  Returns (counter, outputs, wall s, HIP-event ms of
-        every launch on the launch stream)."""
-        kc = C.KmerCounter(k, dev)
-        outs = [kc.alloc_out(db.n) if db is not None else None for db in dbs]
-
-        def step(evs=None):
-            for db, o in zip(dbs, outs):
-                if db is None:
-                    continue
-                if evs is not None:
-                    e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                    e[0].record(stream)
-                kc.count(db, o[0], o[1], accumulate=False)   # the CLI's call
-                if evs is not None:
-                    e[1].record(stream)
-                    evs.append(e)
-
-        for _ in range(warmup):
-            step()
-        torch.cuda.synchronize(dev)
-        evs = []
-        barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step(evs)
-        torch.cuda.synchronize(dev)
-        barrier()
-        el = time.perf_counter() - t0
-        return kc, outs, el, [a.elapsed_time(b) for a, b in evs]
-
-    def verify(k, j, outs, picks):
-        """totals are analytic for N-free synthetic genomes; `picks` genomes of
-        sub-batch j bit-exact vs the oracle (the checker, outside the timed region)"""
-        a, st, c = plan[j]
-        ok = True
-        for o in outs:
-            if o is None:
-                continue
-            ok &= bool((o[1].cpu().numpy() == args.seq_len - k + 1).all())
-        if picks and c:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import kf_oracle as O
-            cnp = C.counts_to_numpy(outs[0][0])
-            for i in np.linspace(0, c - 1, min(picks, c)).astype(int):
-                g = a + int(i) * st
-                cc, t = O.count(O.synth_genome(g, SEED + g, args.seq_len, 80), k)
-                ok &= bool((cnp[i] == cc).all()) and int(outs[0][1][i]) == t
-        return ok
-
-    def all_ok(ok):
-        if world > 1:
-            f = torch.tensor([0.0 if ok else 1.0], device=dev if not rehearse else "cpu")
-            dist.all_reduce(f, op=dist.ReduceOp.MAX)
-            ok = float(f) == 0.0
-        return ok
-
-    def max_over_ranks(*v):
-        if world == 1:
-            return v
-        t = torch.tensor(v, dtype=torch.float64, device=dev if not rehearse else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return tuple(float(x) for x in t)
-
-    ok = True
-    launch_ms = []
-    if resident:
-        dbs = [gen(j) for j in range(len(plan))]
-        kc, outs, el, launch_ms = run(args.k, args.steps, args.warmup, dbs)
-        ok &= verify(args.k, 0, outs[:1], args.verify)
-        for j in range(1, len(plan)):
-            ok &= verify(args.k, j, [outs[j]], 0)
-        del outs
-    else:
-        el = 0.0
-        dbs = None
-        for j in range(len(plan)):
-            db = gen(j)
-            kc, outs, e, ms = run(args.k, args.steps, args.warmup, [db])
-            el += e
-            launch_ms += ms
-            ok &= verify(args.k, j, outs, args.verify if j == 0 else 0)
-            del outs, db
-    kern_ms = float(np.mean(launch_ms)) if launch_ms else 0.0
-    el, kern_ms = max_over_ranks(el, kern_ms)
-    ok = all_ok(ok)
-    ceiling = stream_ceiling(torch, dbs[0].data, stream) if (rank == 0 and resident and dbs and dbs[0] is not None) \
-        else None
-    nsb = sum(1 for _, _, c in plan if c)
+    m = W.measure(args.k, args.steps, args.warmup, resident, args.verify, keep=True, pre=prewarm)
+    ok = m["ok"]
+    kc, dbs = m["kc"], m["dbs"]
+    kern_ms = float(np.mean(m["launch_ms"])) if m["launch_ms"] else 0.0
+    el, kern_ms = W.max_over_ranks(m["el"], kern_ms)
+    ok = W.all_ok(ok)
+    first = dbs[0] if dbs else None
+    cold = cold_launch_ms(torch, kc, first, stream) if (rank == 0 and first is not None) else None
+    nsb = W.nsb
+    n = W.n
     # per launch (one sub-batch): FASTA bytes read + 4 B x bins written (SURVEY 8(d))
-    alg_bytes = (fasta_bytes + 4 * kc.nbins * n) / max(1, nsb)
+    alg_bytes = (W.fasta_bytes + 4 * kc.nbins * n) / max(1, nsb)
     grid, block, lds = kc.launch_info()
 
-    total_bases = bases * world if workload == "configs1" else args.total_genomes * args.seq_len
+    total_bases = bases * world if W.kind == "configs1" else args.total_genomes * args.seq_len
     value = total_bases / el * args.steps / 1e9
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms else 0.0
     workload_tag = f"{n // max(1, nsb)} synthetic {args.seq_len / 1e6:g} Mbp genomes, 80-column FASTA"
     traffic, traffic_src = load_traffic(args.k, workload_tag)
-    if workload == "configs1":
+    if W.kind == "configs1":
         wl = (f"{world}xMI355X, k={args.k}, {args.genomes_per_gpu} synthetic {args.seq_len / 1e6:g} Mbp genomes per GPU"
               + (" (BASELINE configs[1])" if world == 1 else " (configs[1] batch on every GPU, weak)"))
         cfg = {"workload": wl, "k": args.k, "genomes_per_gpu": args.genomes_per_gpu, "seq_len": args.seq_len,
@@ -375,6 +581,7 @@ def main() -> None:
                "sub_batch": args.sub_batch, "resident": resident,
                "parallelism": f"round-robin genome shards x{world}, no collective"}
     cfg.update({"kernel_grid": [grid, block], "lds_bytes": lds})
+    wm = m["warm_ms"]
     out = {
         "metric": "Gbases/s k-mer→.kf build at k=7; achieved HBM GB/s vs gfx950 peak",
         "value": round(value, 3),
@@ -384,7 +591,7 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak" if workload == "configs1" else "strong",
+        "scaling": "weak" if W.kind == "configs1" else "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (device-generated, seeded splitmix64; no datasets)",
@@ -394,17 +601,24 @@ def main() -> None:
                      "traffic_source": traffic_src, "per_gpu": True,
                      "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": int(alg_bytes),
                      "aggregate_achieved": round(achieved * world, 1),
-                     "measured_ceiling": ceiling},
+                     "cold_kernel_ms": round(cold, 4) if cold is not None else None,
+                     "warmup_kernel_ms": [round(x, 4) for x in wm],
+                     "measured_ceiling": ceiling or None},
+        "prewarm": ("measured_ceiling probes before the warmup steps: kf_stream_probe x{} + {} D2D copies of the "
+                    "batch (~70 ms of HBM streaming; clocks settle over the first ~20-30 ms of sustained load, "
+                    "profiles/r04/v1_cold.json)".format(ceiling.get("probe_reps"), ceiling.get("copy_reps"))
+                    if ceiling else None),
         "parity": "ok" if ok else "MISMATCH",
+        "build_id": N.build_id(),
     }
     if args.secondary_k and world == 1 and args.secondary_k != args.k and resident:
         k2 = args.secondary_k
         st2 = max(3, args.steps // 4)
-        kc2, o2, el2, ms2 = run(k2, st2, 1, dbs)
-        ok2 = verify(k2, 0, o2, args.verify)
+        kc2, o2, el2, ms2, _ = W.run(k2, st2, 1, dbs)
+        ok2 = W.verify(k2, 0, o2, args.verify)
         ok &= ok2
         km2 = float(np.mean(ms2))
-        alg2 = (fasta_bytes + 4 * kc2.nbins * n) / max(1, nsb)
+        alg2 = (W.fasta_bytes + 4 * kc2.nbins * n) / max(1, nsb)
         tr2, src2 = load_traffic(k2, workload_tag)
         out["secondary"] = {
             "config": f"1xMI355X, k={k2} (BASELINE configs[4]), same batch",
@@ -417,8 +631,14 @@ def main() -> None:
             "parity": "ok" if ok2 else "MISMATCH"}
         out["parity"] = "ok" if ok else "MISMATCH"
         del o2
+    del dbs, first, m
+    if rank == 0 and world == 1 and args.e2e_genomes:
+        torch.cuda.empty_cache()
+        out["e2e"] = e2e_bench(args, dev)
+        ok &= out["e2e"]["parity"] == "ok"
+        out["parity"] = "ok" if ok else "MISMATCH"
     if rank == 0 and world == 1 and not args.no_cpu:
-        ids = [a + i * st for a, st, c in plan for i in range(c)]
+        ids = [a + i * st for a, st, c in W.plan for i in range(c)]
         out["cpu_baseline"] = cpu_baseline(args, ids)
     if rank == 0:
         print(json.dumps(out), flush=True)

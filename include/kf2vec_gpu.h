@@ -15,7 +15,10 @@
  *   - plain pointers and sizes only; `d_` pointers are device (HBM) pointers,
  *     e.g. `torch.Tensor.data_ptr()` of a ROCm tensor; the CALLER owns every buffer;
  *   - `stream` is a hipStream_t (NULL = default stream); device entry points only
- *     enqueue work (no host sync, no allocation) so they can be graph-captured;
+ *     enqueue work, so they can be graph-captured -- with one exception:
+ *     kf_count_batch at k >= 9 allocates the library's workspace on first use
+ *     and grows its piece table (a device sync) when n_genomes exceeds every
+ *     earlier call; kf_workspace_reserve() does both up front;
  *   - return 0 on success, a negative KF_E* code on failure; the message is in
  *     kf_last_error() (thread-local).  Errors are never silent (deliberate
  *     deviation from main.py:309-311, which discards Jellyfish's stderr/status).
@@ -97,24 +100,39 @@ int kf_index_records(const uint8_t* bytes, uint64_t len, int fmt, uint64_t base,
  *                flags & KF_ACCUMULATE
  *   d_totals   : n_genomes uint64, number of k-mers counted per genome
  * Asynchronous on `stream`.  For k >= 9 the library counts through a device
- * workspace it allocates on first use (about 9 GB on a 256-CU device: 2 bytes
- * of sorted records per byte of the 8 MiB genome piece each CU holds, in two
- * slots for the staggered phases) and keeps
- * until kf_workspace_release(); launches on different streams of one device
- * that use it are ordered by the library. */
+ * workspace (about 9 GB on a 256-CU device: 2 bytes of sorted records per byte
+ * of the 8 MiB genome piece each CU holds, in two slots for the staggered
+ * phases) plus a piece table of n_genomes+1 words, kept until
+ * kf_workspace_release().  Both are allocated on first use; the piece table is
+ * re-allocated behind a hipDeviceSynchronize() when n_genomes exceeds its
+ * capacity (it grows at least 2x).  Call kf_workspace_reserve() first to keep
+ * every kf_count_batch asynchronous and allocation-free.  Launches on different
+ * streams of one device that use the workspace are ordered by the library. */
 int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
                    const uint64_t* d_excl, uint64_t n_excl,
                    const uint32_t* d_code2col, const uint32_t* d_col2rep, int k,
                    uint32_t* d_counts, uint64_t* d_totals, uint32_t flags, void* stream);
 
+/* Allocate up front, on the current device, everything kf_count_batch(k, n)
+ * needs for any n <= max_genomes: the k >= 9 bucket tables, workspace and piece
+ * table, and the kernel attributes of k.  Afterwards such calls neither
+ * allocate nor synchronise.  Synchronous; may be called again with a larger
+ * max_genomes. */
+int kf_workspace_reserve(int k, int32_t max_genomes);
+
 /* Grid the count kernel will use on the current device for k (workgroups,
  * threads per workgroup, dynamic LDS bytes); for roofline accounting.
- * Kernel choice: k = 7 K1x (KF_COUNT_VARIANT 19), k = 8 its single-pass form
- * (24), k <= 6 K1 (1), k >= 9 the bucket kernels; KF_COUNT_VARIANT selects the
- * measured alternatives (kf_count.hip lists them), for A/B runs only.  Variants
- * 22 and 23 keep one small per-workgroup claim buffer per device and stream,
- * allocated on first use. */
+ * Kernel choice: k <= 6 K1 (k1_kernel), k = 7 the pair kernel K1x
+ * (k1x_kernel<7>), k = 8 its single-pass form (k1x_kernel<8>), k >= 9 the
+ * two-phase bucket kernels (bucket_kernel<k>).  No environment variable
+ * changes the choice. */
 int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
+
+/* Hash of the sources this library was built from (csrc/ + this header, as
+ * kf2vecfsw_amd/build.py computes it): 16 hex digits, with a "+<tag>" suffix for
+ * profiling builds.  The Python binding refuses a library whose id differs from
+ * the sources next to it. */
+const char* kf_build_id(void);
 
 /* Measurement aid (bench.py): read d_bytes[0, n) with the fastest read pattern
  * measured on gfx950 (3 KiB blocks dealt grid-stride over the waves, coalesced

@@ -39,6 +39,8 @@ SIGNATURES = {
     "kf_count_batch": (_int, [_vp, _vp, _i32, _vp, _u64, _vp, _vp, _int, _vp, _vp, _u32, _vp]),
     "kf_count_launch_info": (_int, [_int, _PI, _PI, _PI]),
     "kf_workspace_release": (_int, []),
+    "kf_workspace_reserve": (_int, [_int, _i32]),
+    "kf_build_id": (_cp, []),
     "kf_stream_probe": (_int, [_vp, _u64, _vp, _vp]),
     "kf_synth_fasta": (_int, [_vp, _vp, _i32, _i64, _i64, _u64, _u64, _int, _u64, _vp]),
     "kf_synth_genome_bytes": (_u64, [_i64, _u64, _int, _u64]),
@@ -80,8 +82,21 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         if L.kf_abi_version() != 1:
             raise NativeError("libkf2vec_gpu ABI version mismatch")
+        bid = L.kf_build_id().decode()
+        if not os.environ.get("KF2VEC_GPU_LIB"):
+            # the product library must be built from the sources next to it
+            # (it travels prebuilt with repo snapshots; build.source_id)
+            from .build import source_id
+            if bid != source_id():
+                raise NativeError(f"{LIB_PATH} was built from other sources (build id {bid}, sources "
+                                  f"{source_id()}): rebuild with `python -m kf2vecfsw_amd.build`")
         _lib = L
     return _lib
+
+
+def build_id() -> str:
+    """kf_build_id() of the loaded library (hash of its sources)."""
+    return lib().kf_build_id().decode()
 
 
 def check(rc: int, what: str = "") -> None:

@@ -6,6 +6,7 @@ to the GPU box with the repo snapshot.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -22,11 +23,35 @@ SOURCES_CPP = ["kf_host.cpp"]
 DEPS = SOURCES_HIP + SOURCES_CPP + ["kf_internal.h", "kf_front.h", "../../include/kf2vec_gpu.h"]
 
 
+def source_id() -> str:
+    """Hash of the library's sources (csrc/ + the C-ABI header) and target: what
+    kf_build_id() of a library built from them returns (16 hex digits)."""
+    h = hashlib.sha256(ARCH.encode())
+    for d in sorted(DEPS):
+        h.update(b"\0" + os.path.basename(d).encode() + b"\0")
+        with open(os.path.join(CSRC, d), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def embedded_id(path: str) -> str | None:
+    """The build id embedded in a built library (without loading it)."""
+    try:
+        with open(path, "rb") as f:
+            blob = f.read()
+    except OSError:
+        return None
+    i = blob.find(b"KF_BUILD_ID=")
+    if i < 0:
+        return None
+    j = blob.find(b"\0", i)
+    return blob[i + 12: j].decode(errors="replace")
+
+
 def _stale() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(os.path.join(CSRC, d)) > t for d in DEPS)
+    """The product library is stale unless its embedded id equals the sources'
+    hash (mtimes are not trusted: the .so travels with repo snapshots)."""
+    return embedded_id(OUT) != source_id()
 
 
 def build(force: bool = False, verbose: bool = False, ablation: bool = False, out: str | None = None) -> str:
@@ -47,6 +72,10 @@ def build(force: bool = False, verbose: bool = False, ablation: bool = False, ou
 
 def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
     objs = []
+    # profiling / ablation builds carry a suffix, so the product check refuses them
+    flags = os.environ.get("KF_HIPCC_FLAGS", "")
+    bid = source_id() + ("+prof" if ablation else "") + \
+        ("+flags" + hashlib.sha256(flags.encode()).hexdigest()[:8] if flags.strip() else "")
     for s in SOURCES_HIP:
         o = os.path.join(BUILD, s + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
@@ -59,7 +88,7 @@ def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
     for s in SOURCES_CPP:
         o = os.path.join(BUILD, s + ".o")
         subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-pthread",
-                        "-c", os.path.join(CSRC, s), "-o", o], check=True)
+                        f'-DKF_BUILD_ID="{bid}"', "-c", os.path.join(CSRC, s), "-o", o], check=True)
         objs.append(o)
     tmp = out + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs, "-o", tmp],

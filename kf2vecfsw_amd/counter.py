@@ -218,6 +218,12 @@ class KmerCounter:
                     "kf_count_launch_info")
         return g.value, b.value, l.value
 
+    def reserve(self, max_genomes: int) -> None:
+        """Allocate the library's workspace for batches of up to max_genomes now
+        (kf_workspace_reserve), so that count() never allocates or synchronises."""
+        with torch.cuda.device(self.device):
+            N.check(N.lib().kf_workspace_reserve(self.k, int(max_genomes)), "kf_workspace_reserve")
+
     def alloc_out(self, n: int) -> tuple[torch.Tensor, torch.Tensor]:
         return (torch.empty((n, self.nbins), dtype=torch.int32, device=self.device),
                 torch.empty(n, dtype=torch.int64, device=self.device))

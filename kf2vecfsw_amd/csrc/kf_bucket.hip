@@ -1032,6 +1032,22 @@ int ensure_tables(DevState& d, int k) {
     return KF_OK;
 }
 
+// Scratch of one device: records, round metadata, round offsets, sized for the
+// largest of the compiled geometries (so a launch at another k reuses it).
+void scratch_layout(int cus, size_t& rec_b, size_t& meta_b, size_t& roff_b) {
+    rec_b = meta_b = roff_b = 0;
+    for (int kk = 9; kk <= KF_MAX_K; ++kk) {   // the bucket kernels: k >= 9
+        const size_t g = (size_t)cus * (16 / bucket_waves_for(kk)) * kBkSlots;
+        bucket_geom(kk, [&](auto b) {
+            using Lk = decltype(b);
+            rec_b = std::max(rec_b, g * (size_t)Lk::rec_cap * 2);
+            meta_b = std::max(meta_b, g * ((size_t)Lk::nbk + 1) * Lk::rmax * 2);
+            roff_b = std::max(roff_b, g * (size_t)Lk::rmax * 4);
+            return 0;
+        });
+    }
+}
+
 }  // namespace
 
 namespace kf {
@@ -1047,47 +1063,30 @@ int bucket_launch_info(int k, int* grid, int* block, int* lds) {
     return KF_OK;
 }
 
-int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
-    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
+// Everything a launch at k over n_genomes needs on device `dev` (caller holds
+// g_mu): the bucket tables of k, the kernel's LDS attribute, the scratch (sized
+// for the largest compiled geometry, so every k shares it) and a piece table of
+// at least n_genomes+1 words (grown 2x at a time; a regrowth synchronises the
+// device, since a launch in flight may still read the old one).
+int ensure_workspace(DevState& d, int dev, int k, int32_t n_genomes) {
     void* fn = bucket_kernel_for(k);
     if (!fn) return kf_fail(KF_EINVAL, "no bucket kernel for k=%d", k);
-    std::lock_guard<std::mutex> lk(g_mu);
-    DevState& d = g_dev[dev];
     int rc = ensure_tables(d, k);
     if (rc) return rc;
     const uint32_t lds = bucket_lds_for(k);
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     if (!d.cus) {
-        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-            return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return kf_fail(KF_EHIP, "hipDeviceGetAttribute(MultiprocessorCount) failed");
         d.cus = cus > 0 ? cus : 1;
         if (hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess)
             return kf_fail(KF_EHIP, "hipEventCreate failed");
-    } else if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
-        return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     }
-    const int waves = bucket_waves_for(k);
-    const int grid = d.cus * (16 / waves);   // 16 waves per CU
-    // scratch: records, round metadata, round offsets (sized for the largest of
-    // the compiled geometries, so that a launch at another k reuses it)
     size_t rec_b = 0, meta_b = 0, roff_b = 0;
-    for (int kk = 9; kk <= KF_MAX_K; ++kk) {   // the bucket kernels: k >= 9
-        const size_t g = (size_t)d.cus * (16 / bucket_waves_for(kk)) * kBkSlots;
-        bucket_geom(kk, [&](auto b) {
-            using Lk = decltype(b);
-            rec_b = std::max(rec_b, g * (size_t)Lk::rec_cap * 2);
-            meta_b = std::max(meta_b, g * ((size_t)Lk::nbk + 1) * Lk::rmax * 2);
-            roff_b = std::max(roff_b, g * (size_t)Lk::rmax * 4);
-            return 0;
-        });
-    }
+    scratch_layout(d.cus, rec_b, meta_b, roff_b);
     const size_t need = rec_b + meta_b + roff_b;
-    if (d.done && hipStreamWaitEvent(s, d.done, 0) != hipSuccess)
-        return kf_fail(KF_EHIP, "hipStreamWaitEvent failed");
     if (d.scratch_bytes < need) {
         if (d.scratch && (hipDeviceSynchronize() != hipSuccess || hipFree(d.scratch) != hipSuccess))
             return kf_fail(KF_EHIP, "hipFree of bucket scratch failed");
@@ -1097,15 +1096,44 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
             return kf_fail(KF_EHIP, "hipMalloc of %zu bytes of bucket scratch failed", need);
         d.scratch_bytes = need;
     }
-    if (d.pstart_n < (size_t)A.n_genomes + 1) {
+    if (d.pstart_n < (size_t)n_genomes + 1) {
+        const size_t cap = std::max((size_t)n_genomes + 1, 2 * d.pstart_n);
         if (d.pstart && (hipDeviceSynchronize() != hipSuccess || hipFree(d.pstart) != hipSuccess))
             return kf_fail(KF_EHIP, "hipFree of piece table failed");
         d.pstart = nullptr;
         d.pstart_n = 0;
-        if (hipMalloc((void**)&d.pstart, ((size_t)A.n_genomes + 1) * 4) != hipSuccess)
+        if (hipMalloc((void**)&d.pstart, cap * 4) != hipSuccess)
             return kf_fail(KF_EHIP, "hipMalloc of piece table failed");
-        d.pstart_n = (size_t)A.n_genomes + 1;
+        d.pstart_n = cap;
     }
+    return KF_OK;
+}
+
+int bucket_reserve(int k, int32_t max_genomes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
+    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_mu);
+    return ensure_workspace(g_dev[dev], dev, k, max_genomes);
+}
+
+int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
+    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
+    void* fn = bucket_kernel_for(k);
+    if (!fn) return kf_fail(KF_EINVAL, "no bucket kernel for k=%d", k);
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevState& d = g_dev[dev];
+    int rc = ensure_workspace(d, dev, k, A.n_genomes);
+    if (rc) return rc;
+    const uint32_t lds = bucket_lds_for(k);
+    const int waves = bucket_waves_for(k);
+    const int grid = d.cus * (16 / waves);   // 16 waves per CU
+    size_t rec_b = 0, meta_b = 0, roff_b = 0;
+    scratch_layout(d.cus, rec_b, meta_b, roff_b);
+    if (d.done && hipStreamWaitEvent(s, d.done, 0) != hipSuccess)
+        return kf_fail(KF_EHIP, "hipStreamWaitEvent failed");
     BucketArgs B;
     B.col_idx = d.col_idx[k];
     B.bcol = d.bcol[k];

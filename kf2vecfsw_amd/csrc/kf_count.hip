@@ -21,12 +21,15 @@
 // Kernels:
 //   K1  k1_kernel<K>   (k <= 6): 16-byte lanes, 1 KiB per wave iteration, one
 //       ds_add_u32 per window into a 4^k u32 histogram, two workgroups per CU;
-//   K1x k1x_kernel<7>  (k = 7): 48-byte lanes, 3 KiB per wave iteration; two
-//       consecutive 7-mer windows are one 8-mer counted once in P (65,536 u16
-//       counters, 128 KiB), a window left unpaired goes to S (16,384 u16 by
-//       forward 7-mer, 32 KiB): half the LDS atomics of K1; every add returns
-//       the old word and a u16 half that reaches 0x4000 is moved to the count
-//       row (exact: see x_fast);
+//   K1x k1x_kernel<7>  (k = 7): 3 KiB per wave iteration read as three
+//       coalesced 1 KiB regions (lane L: bytes 16L + 1024q, non-temporal
+//       buffer loads, xc_load); windows are formed per 16-byte region, the
+//       k-1 bases of context from lane L-1 by DPP.  Two consecutive 7-mer
+//       windows are one 8-mer counted once in P (65,536 u16 counters,
+//       128 KiB), a window left unpaired goes to S (16,384 u16 by forward
+//       7-mer, 32 KiB): half the LDS atomics of K1; every add returns the old
+//       word and a u16 half that reaches 0x4000 is moved to the count row
+//       (exact: see xc_fast);
 //   K1x8 k1x_kernel<8> (k = 8): the K1x front end with every window an 8-mer
 //       in P (one pass over the bytes).
 // Rejected alternatives and their measurements live in tools/zoo/ (DESIGN.md).
@@ -233,7 +236,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 
 constexpr uint32_t kPBytes = 1u << 17;                 // byte offset of S
 constexpr uint32_t kXLdsBytes = kPBytes + (1u << 15);  // 160 KiB
 constexpr int kXChunk = 3 * kChunk;                    // bytes per wave iteration
-// u16 exactness (x_fast): k = 7 checks every add's return against 0x4000 and
+// u16 exactness (xc_fast): k = 7 checks every add's return against 0x4000 and
 // moves 0x4000 at a time; k = 8 (48 adds per lane per iteration) against 0x2000.
 constexpr uint32_t kHot7 = 0xC000C000u, kStep7 = 0x4000u;
 constexpr uint32_t kHot8 = 0xE000E000u, kStep8 = 0x2000u;
@@ -317,27 +320,8 @@ constexpr uint32_t kXTabLo = 0x630B6102u;   // e0..e3 = 0x02, 'a', 0x0B, 'c'
 constexpr uint32_t kXTabHi = 0x67000074u;   // e4..e7 = 't', 0x00, 0x00, 'g'
 
 struct XBlock {
-    uint4 q[3];   // lane L: bytes [48L + 16 i, 48L + 16 i + 16) of the 3 KiB iteration
+    uint4 q[3];   // lane L: bytes [16L + 1024 i, 16L + 1024 i + 16) of the 3 KiB iteration
 };
-__device__ __forceinline__ XBlock x_load(const uint8_t* bytes, uint64_t c0, uint32_t rel, uint32_t end_r, int lane) {
-    // clamped to the genome end rounded up to 16 B (load_chunk): bytes past it read 0
-    const uint32_t rec = end_r > rel ? min(end_r - rel, (uint32_t)kXChunk) : 0u;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + c0 + rel), (short)0, (int)rec, 0x00020000);
-    XBlock b;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 48 + 16 * i, 0, 0);
-        b.q[i] = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-    return b;
-}
-
-// dot4 weights of word i's bytes t = 0..3 in the newline test: 2 (96 - (4i + t))
-__device__ __forceinline__ constexpr uint32_t x_nl_weights(int i) {
-    return (uint32_t)(192 - 8 * i) | (uint32_t)(190 - 8 * i) << 8 | (uint32_t)(188 - 8 * i) << 16 |
-           (uint32_t)(186 - 8 * i) << 24;
-}
-
 // z = bits other than 5 (c = 1): x ^ e; bit 5 (c = 0): x & ~e  (one v_bitop3)
 __device__ __forceinline__ uint32_t x_zmap(uint32_t x, uint32_t e, uint32_t c) {
     uint32_t r;
@@ -345,179 +329,15 @@ __device__ __forceinline__ uint32_t x_zmap(uint32_t x, uint32_t e, uint32_t c) {
     return r;
 }
 
-// Classification of a 3 KiB block: the packed codes of each lane's 48 bytes
-// (newline entry not yet removed) and the newline / bad-byte sum V.
-struct XCls {
-    uint32_t C[3], V;
-};
-__device__ __forceinline__ XCls x_cls(const XBlock& d) {
-    const uint32_t w[12] = {d.q[0].x, d.q[0].y, d.q[0].z, d.q[0].w, d.q[1].x, d.q[1].y,
-                            d.q[1].z, d.q[1].w, d.q[2].x, d.q[2].y, d.q[2].z, d.q[2].w};
-    const uint32_t cdf = 0xDFDFDFDFu;
-    uint32_t pc[12], z[12];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-        const uint32_t x = w[i];
-        const uint32_t e = __builtin_amdgcn_perm(kXTabHi, kXTabLo, x & 0x07070707u);
-        z[i] = x_zmap(x, e, cdf);
-        // 2 x packed codes; odd words accumulate onto the even word's, shifted up one byte
-        pc[i] = __builtin_amdgcn_udot4(x & 0x06060606u, 0x01041040u, (i & 1) ? pc[i - 1] << 8 : 0u, false);
-    }
-    // codes: C2 = entries 32..47 (bytes 0..15), C1 = 16..31, C0 = 0..15 (entry 0 = byte 47)
-    uint32_t C[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int b = 4 * (2 - i);
-        C[i] = (pc[b + 1] << 15) | (pc[b + 3] >> 1);
-    }
-    // Newline and bad-byte test in one dot4 chain: byte b (entry 47 - b) weighs
-    // 2 (96 - b), so V = sum z_b 2 (96 - b) is 0 without a newline, 98 + 2e for
-    // one newline at entry e, and >= 196 otherwise (every nonzero z adds >= 98:
-    // two newlines, or one bad byte's z >= 2).
-    uint32_t va[4] = {0u, 0u, 0u, 0u};   // four chains of three: a short dependent path
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) va[c] = __builtin_amdgcn_udot4(z[3 * c + i], x_nl_weights(3 * c + i), va[c], false);
-    XCls r;
-    r.C[0] = C[0], r.C[1] = C[1], r.C[2] = C[2], r.V = (va[0] + va[1]) + (va[2] + va[3]);
-    return r;
-}
-
-// The lane's window register W after the newline entry is removed, with the
-// context from lane L-1 (lane 0: the carry) above this lane's 48 - nl entries:
-// W = pC << 2(48 - nl) | (c2 : c1 : c0), as four words.
-struct XWin {
-    uint32_t w[4], nl;
-};
-__device__ __forceinline__ XWin x_window(const XCls& k, uint32_t carry) {
-    const uint32_t V = k.V;
-    const uint32_t C[3] = {k.C[0], k.C[1], k.C[2]};
-    uint32_t nl;   // min(V, 1), opaque: the compiler would turn its uses into selects (v_cndmask)
-    asm("v_min_u32_e32 %0, 1, %1" : "=v"(nl) : "v"(V));
-    // drop the newline entry: entries below it stay, every entry above moves down
-    // one.  Region r (entries 16r..16r+15) keeps its low q_r = clamp(2e - 32r, 0, 32)
-    // bits; without a newline V - 98 wraps high and every region keeps all.
-    const uint32_t e2 = V - 98u;
-    const uint32_t q0 = min(e2, 32u), q1 = min(max(e2, 32u), 64u) - 32u, q2 = min(max(e2, 64u) - 64u, 32u);
-    const uint32_t L0 = (uint32_t)(~0ull << q0), L1 = (uint32_t)(~0ull << q1), L2 = (uint32_t)(~0ull << q2);
-    const uint32_t c0 = bfi(L0, __builtin_amdgcn_alignbit(C[1], C[0], 2), C[0]);
-    const uint32_t c1 = bfi(L1, __builtin_amdgcn_alignbit(C[2], C[1], 2), C[1]);
-    const uint32_t c2 = bfi(L2, C[2] >> 2, C[2]);
-    const uint32_t pC = wave_shr1(t_codes(carry), c0);
-    const uint64_t t = (uint64_t)pC << (32u - 2u * nl);
-    XWin x;
-    x.w[0] = c0, x.w[1] = c1, x.w[2] = c2 | (uint32_t)t, x.w[3] = (uint32_t)(t >> 32), x.nl = nl;
-    return x;
-}
-
-// k = 7 counting half of a fast iteration: 24 pair adds (23 + window 46 as a
-// single into S when the lane holds a newline).  Returns the OR of the adds'
-// returns for the caller's u16 test; updates the carry.
-__device__ __forceinline__ uint32_t x_body7(const XCls& k, uint32_t& carry, uint32_t& lane_total) {
-    constexpr uint32_t TM = (1u << 12) - 1u;
-    const XWin x = x_window(k, carry);
-    const uint32_t w0 = x.w[0], w1 = x.w[1], w2 = x.w[2], w3 = x.w[3], nl = x.nl;
-    // pair j = windows 2j (newer) and 2j+1 = the 8-mer at bits [4j, 4j+16) of W:
-    // P word address = (X >> 4j) & 0x1FFFC with X = W << 1; half = bit 4j of W.
-    // Views: X dwords and X >> 16 (Y), so every pair is a plain shift and an and.
-    const uint32_t x0 = w0 << 1, x1 = __builtin_amdgcn_alignbit(w1, w0, 31), x2 = __builtin_amdgcn_alignbit(w2, w1, 31),
-                   x3 = __builtin_amdgcn_alignbit(w3, w2, 31);
-    const uint32_t X[3] = {x0, x1, x2};
-    const uint32_t Y[3] = {__builtin_amdgcn_alignbit(x1, x0, 16), __builtin_amdgcn_alignbit(x2, x1, 16),
-                           __builtin_amdgcn_alignbit(x3, x2, 16)};
-    const uint32_t Wd[3] = {w0, w1, w2};
-    constexpr uint32_t PM = 0x1FFFCu;
-    const uint32_t one = 1u;
-    uint32_t rt[24];
-#pragma unroll
-    for (int j = 0; j < 23; ++j) {
-        const int i = j >> 3, tt = j & 7;
-        const uint32_t a = ((tt < 4 ? X[i] : Y[i]) >> (4 * (tt & 3))) & PM;
-        const uint32_t H = (tt & 1) ? (Wd[i] & 0x10101010u) : ((Wd[i] << 4) & 0x10101010u);
-        uint32_t dl;
-        switch (tt >> 1) {
-        case 0: dl = shl1_byte<0>(H, one); break;
-        case 1: dl = shl1_byte<1>(H, one); break;
-        case 2: dl = shl1_byte<2>(H, one); break;
-        default: dl = shl1_byte<3>(H, one); break;
-        }
-        rt[j] = lds_add_rtn(a, dl);
-    }
-    {
-        // pair 23 (windows 46, 47) without a newline; with one, window 46 alone
-        // into S by its forward code y = bits [92, 106) of W.  Both addresses come
-        // from one view: v = X >> 92, P address v & 0x1FFFC, S address
-        // kPBytes | (v & 0x7FFC) (= (y >> 1) << 2); both halves are bit 92 of W.
-        const uint32_t v = Y[2] >> 12;
-        const uint32_t sel = 0u - nl;
-        const uint32_t a23 = bfi(sel, kPBytes | (v & 0x7FFCu), v & PM);
-        rt[23] = lds_add_rtn(a23, shl1_byte<3>(w2 & 0x10101010u, one));
-    }
-    lane_total -= nl;   // + 48 per fast iteration, added by the caller
-    uint32_t o = 0;
-#pragma unroll
-    for (int j = 0; j < 24; j += 3) o |= rt[j] | rt[j + 1] | rt[j + 2];
-    carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)w0, kWave - 1) & TM, 31u, 31u);
-    return o;
-}
-
-// k = 8 counting half of a fast iteration with every window an 8-mer in P:
-// window r = bits [2r, 2r + 16) of W, address (X >> 2r) & 0x1FFFC with X = W << 1,
-// half = W bit 2r.  48 adds per lane (47 with a newline: window 47 then adds 0).
-__device__ __forceinline__ uint32_t x_body8(const XCls& k, uint32_t& carry, uint32_t& lane_total) {
-    constexpr uint32_t TM = (1u << 14) - 1u;   // 7 context entries
-    const XWin x = x_window(k, carry);
-    const uint32_t w0 = x.w[0], w1 = x.w[1], w2 = x.w[2], w3 = x.w[3], nl = x.nl;
-    const uint32_t x0 = w0 << 1, x1 = __builtin_amdgcn_alignbit(w1, w0, 31), x2 = __builtin_amdgcn_alignbit(w2, w1, 31),
-                   x3 = __builtin_amdgcn_alignbit(w3, w2, 31);
-    const uint32_t X[3] = {x0, x1, x2};
-    const uint32_t Y[3] = {__builtin_amdgcn_alignbit(x1, x0, 16), __builtin_amdgcn_alignbit(x2, x1, 16),
-                           __builtin_amdgcn_alignbit(x3, x2, 16)};
-    const uint32_t Wd[3] = {w0, w1, w2};
-    constexpr uint32_t PM = 0x1FFFCu;
-    const uint32_t one = 1u;
-    const uint32_t keep47 = nl - 1u;   // 0 with a newline: window 47 is lane L-1's window 0
-    uint32_t o = 0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        uint32_t rt[24];
-#pragma unroll
-        for (int q = 0; q < 24; ++q) {
-            const int r = 24 * h + q, i = r >> 4, tt = r & 15;
-            const uint32_t a = ((tt < 8 ? X[i] : Y[i]) >> (2 * (tt & 7))) & PM;
-            const int tb = tt & 3;   // W bit 2r sits at bit 8m + 2tb of Wd[i] (m = tt >> 2): move it to 8m + 4
-            const uint32_t H = (tb == 0 ? Wd[i] << 4 : (tb == 1 ? Wd[i] << 2 : (tb == 2 ? Wd[i] : Wd[i] >> 2))) & 0x10101010u;
-            uint32_t dl;
-            switch (tt >> 2) {
-            case 0: dl = shl1_byte<0>(H, one); break;
-            case 1: dl = shl1_byte<1>(H, one); break;
-            case 2: dl = shl1_byte<2>(H, one); break;
-            default: dl = shl1_byte<3>(H, one); break;
-            }
-            if (r == 47) dl &= keep47;
-            rt[q] = lds_add_rtn(a, dl);
-        }
-#pragma unroll
-        for (int q = 0; q < 24; q += 3) o |= rt[q] | rt[q + 1] | rt[q + 2];
-    }
-    lane_total -= nl;
-    carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)w0, kWave - 1) & TM, 31u, 31u);
-    return o;
-}
-
 // ---------------------------------------------------------------- K1x, coalesced layout
-// KF_XC = 1: the 3 KiB iteration is read as three 1 KiB regions, lane L holding
+// The 3 KiB iteration is read as three 1 KiB regions, lane L holding
 // bytes [16L, 16L+16) of each, so every load instruction reads 1 KiB contiguous,
 // with the non-temporal cache policy.  Measured streaming rate of the two layouts
 // (tools/cpol_rate.hip, profiles/r03/v8_cpol_rate.txt): 6.8 TB/s coalesced + nt vs
-// 5.6-5.8 TB/s for 48-byte lanes, which the nt bit slows to 4.5.  Windows are
+// 5.6-5.8 TB/s for rounds 1-2's 48-byte lanes, which the nt bit slows to 4.5.  Windows are
 // formed and paired per 16-byte region: a lane holds 16 entries (15 with a
 // newline), the k-1 entries of context come from lane L-1's region by DPP, lane
 // 0 takes the previous region's lane 63.
-#ifndef KF_XC
-#define KF_XC 1
-#endif
 #ifndef KF_NT_STORES
 #define KF_NT_STORES 1   // non-temporal count-row stores (k=7 -1.4 %; v10_lib_ab_k*_nt_stores)
 #endif
@@ -546,7 +366,9 @@ __device__ __forceinline__ constexpr uint32_t xc_nl_weights(int i) {
 }
 constexpr uint32_t kXcBad = 68u;   // V at or above: not the fast case
 
-// One region's codes (entry 0 = byte 15) and newline / bad-byte sum (as x_cls).
+// One region's codes (entry 0 = byte 15) and newline / bad-byte sum: per dword,
+// the v_perm table lookup and x_zmap above give z, one v_dot4 per dword packs
+// the codes and another sums z weighted by position (xc_nl_weights).
 struct XcCls {
     uint32_t C, V;
 };
@@ -580,7 +402,7 @@ struct XcWin {
     uint32_t x0, y0, c, nl;
 };
 __device__ __forceinline__ XcWin xc_window(const XcCls& k, uint32_t rot) {
-    uint32_t nl;   // min(V, 1), opaque (see x_window)
+    uint32_t nl;   // min(V, 1), opaque: the compiler would turn its uses into selects (v_cndmask)
     asm("v_min_u32_e32 %0, 1, %1" : "=v"(nl) : "v"(k.V));
     const uint32_t q = min(k.V - 34u, 32u);   // 2e; no newline: wraps high, 32
     const uint32_t L = (uint32_t)(~0ull << q);
@@ -647,9 +469,13 @@ __device__ __forceinline__ void xc_wins8(const XcWin& x, uint32_t (&rt)[16]) {
     }
 }
 
-// Fast case of a coalesced 3 KiB iteration (as x_fast): every region of every lane
-// is bases with at most one newline and the carry is complete.  u16 exactness as
-// x_fast: k = 7 adds 24 per lane and iteration, k = 8 48.
+// Fast case of a coalesced 3 KiB iteration (uniform): every region of every lane
+// is bases with at most one newline and the carry is complete; returns false
+// (nothing counted) otherwise.  u16 exactness: every add's return is checked at
+// the end of its iteration; after a half crosses HOT's threshold, every wave adds
+// at most one more iteration to it before its own drain.  k = 7: at most 24 x 64
+// adds per wave and iteration, so a half stays below 0x4000 + 16 x 1536 = 0xA000;
+// k = 8: 48 x 64, below 0x2000 + 16 x 3072 = 0xE000.
 template <int K>
 __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
                                         uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
@@ -684,28 +510,6 @@ __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int
     }
     lane_total -= x0.nl + x1.nl + x2.nl;   // + 48 per fast iteration, added by the caller
     carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)x2.c, kWave - 1) & TM, 31u, 31u);
-    if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
-        x_scan_drain<K>(A.code2col, gcounts, lane);
-        drained = 1;
-    }
-    return true;
-}
-
-// Fast case of a 3 KiB iteration (uniform): every lane's 48 bytes are bases with
-// at most one newline, and the carry is complete; returns false (nothing
-// counted) otherwise.  u16 exactness: every add's return is checked at the end
-// of its iteration; after a half crosses HOT's threshold, every wave adds at most
-// one more iteration to it before its own drain.  k = 7: at most 24 x 64 adds
-// per wave and iteration, so a half stays below 0x4000 + 16 x 1536 = 0xA000;
-// k = 8: 48 x 64, below 0x2000 + 16 x 3072 = 0xE000.
-template <int K>
-__device__ __forceinline__ bool x_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
-                                       uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
-    constexpr uint32_t HOT = K == 8 ? kHot8 : kHot7;
-    const XCls k = x_cls(d);
-    carry = __builtin_amdgcn_readfirstlane(carry);   // wave-uniform: its tests run on the SALU
-    if (t_n(carry) < (uint32_t)(K - 1) || __builtin_amdgcn_ballot_w64(k.V >= 196u) != 0) return false;
-    const uint32_t o = K == 8 ? x_body8(k, carry, lane_total) : x_body7(k, carry, lane_total);
     if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
         x_scan_drain<K>(A.code2col, gcounts, lane);
         drained = 1;
@@ -754,7 +558,7 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
     rg.init(glo, ghi, lo, hi);
     XBlock buf[kXRing];
     auto load = [&](uint32_t r) {
-        return KF_XC ? xc_load(A.bytes, rg.c0, r, rg.end_r, lane) : x_load(A.bytes, rg.c0, r, rg.end_r, lane);
+        return xc_load(A.bytes, rg.c0, r, rg.end_r, lane);
     };
 #pragma unroll
     for (int j = 0; j < kXRing; ++j) buf[j] = load(j * kXChunk);
@@ -770,8 +574,7 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
         // one test for the whole 3 KiB (range edges, excluded intervals)
         bool fast = !rg.masked_span(A, rel, kXChunk);
         if (fast)
-            fast = KF_XC ? xc_fast<K>(bf, A, lane, carry, gcounts, lane_total, drained)
-                         : x_fast<K>(bf, A, lane, carry, gcounts, lane_total, drained);
+            fast = xc_fast<K>(bf, A, lane, carry, gcounts, lane_total, drained);
         nfast += fast ? 1u : 0u;
         if (!fast) {
             // interval cursor before each 1 KiB third (a later test may advance it)
@@ -788,7 +591,7 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
                 const bool mh = h == 0 ? m0 : (h == 1 ? m1 : m2);
                 const uint64_t ivh = h == 0 ? iv0 : (h == 1 ? iv1 : rg.iv);
                 // the coalesced block already holds this third in the 16-byte lane layout
-                const uint4 hb = KF_XC ? bf.q[h] : rg.load(A.bytes, r, lane);
+                const uint4 hb = bf.q[h];
                 if (mh)
                     carry = x_singles<K, true>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
                 else
@@ -1134,6 +937,14 @@ extern "C" int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes
     if (!grid || !block || !lds_bytes) return kf_fail(KF_EINVAL, "null output pointer");
     if (k >= 9) return bucket_launch_info(k, grid, block, lds_bytes);
     return launch_info(k, grid, block, lds_bytes);
+}
+
+extern "C" int kf_workspace_reserve(int k, int32_t max_genomes) {
+    if (k < KF_MIN_K || k > KF_MAX_K) return kf_fail(KF_EINVAL, "k out of range [2, 12]");
+    if (max_genomes < 0) return kf_fail(KF_EINVAL, "max_genomes < 0");
+    if (k >= 9) return bucket_reserve(k, max_genomes);
+    int grid = 0, block = 0, lds = 0;   // the kernel attribute and grid of k
+    return launch_info(k, &grid, &block, &lds);
 }
 
 extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,

@@ -555,5 +555,6 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // written whole (no memset needed unless accumulating); the caller zeroes totals.
 int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s);
 int bucket_launch_info(int k, int* grid, int* block, int* lds);
+int bucket_reserve(int k, int32_t max_genomes);
 
 }  // namespace kf

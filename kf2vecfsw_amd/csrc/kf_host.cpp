@@ -370,3 +370,12 @@ extern "C" uint64_t kf_synth_genome_bytes(int64_t g, uint64_t seq_len, int width
     if (align < 1) align = 1;
     return (need + align - 1) / align * align;
 }
+
+// ------------------------------------------------------------------ build provenance
+#ifndef KF_BUILD_ID
+#define KF_BUILD_ID "unknown"
+#endif
+// "KF_BUILD_ID=<id>" is kept whole in the binary so build.py can read the id
+// without loading the library.
+static const char kBuildId[] = "KF_BUILD_ID=" KF_BUILD_ID;
+extern "C" const char* kf_build_id(void) { return kBuildId + 12; }

@@ -1,0 +1,95 @@
+"""GPU parity of the BASELINE.json workloads themselves:
+
+* configs[1] at full size -- 1,000 synthetic 5 Mbp genomes generated in HBM by
+  kf_synth_fasta (5.06 GB), counted by the k=7 kernel in one kf_count_batch --
+  every genome's 8,192 counts and total bit-exact against the oracle run on the
+  same bytes (OpenMP over the host's CPUs), with and without N runs;
+* configs[3]'s code path -- bench.py's Workload (round-robin shard plan,
+  device-generated sub-batches, resident and streamed modes) in-process at a
+  small total, every genome of every sub-batch checked against the oracle.
+
+The reference counts with Jellyfish (kf2vec/main.py:309-323); the oracle is its
+restatement pinned by the toy goldens (tests/test_oracle_golden.py)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20260101
+
+
+@pytest.fixture(scope="module")
+def torch_dev(native):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests need an MI355X")
+    return torch.device("cuda:0")
+
+
+def host_threads() -> int:
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.usable_cpus()[0]
+
+
+@pytest.mark.parametrize("n_period", [0, 3])
+def test_configs1_full_batch_every_genome(torch_dev, oracle, n_period):
+    """BASELINE configs[1]: 1,000 x 5 Mbp at k=7, every genome bit-exact (n_period=3:
+    N runs of 1-100 bases in about a third of the 4 KiB blocks, which reset k-mers)."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    n, L, k = 1000, 5_000_000, 7
+    db = C.synth_device_batch(n, L, SEED, width=80, n_period=n_period, device=torch_dev)
+    kc = C.KmerCounter(k, torch_dev)
+    cnt, tot = kc.count(db)
+    torch.cuda.synchronize()
+    counts, totals = C.counts_to_numpy(cnt), tot.cpu().numpy()
+    del cnt, tot
+    off = db.off.cpu().numpy().view(np.uint64)
+    host = db.data.cpu().numpy()
+    del db
+    torch.cuda.empty_cache()
+    if n_period == 0:
+        assert (totals == L - k + 1).all()                          # analytic: no N, one record
+    else:
+        assert (totals < L - k + 1).all() and (totals > L // 2).all()
+    # the device generator writes what the oracle's generator writes (first, last,
+    # and genomes around workgroup span boundaries)
+    grid = kc.launch_info()[0]
+    span = int(off[-1]) // grid
+    picks = {0, n - 1} | {int(np.searchsorted(off, b * span, side="right")) - 1 for b in (1, 77, 128, grid - 1)}
+    for i in sorted(picks):
+        exp = oracle.synth_genome(i, SEED + i, L, 80, n_period, int(off[i + 1] - off[i]))
+        assert host[off[i]: off[i + 1]].tobytes() == exp, i
+    # every genome against the oracle on the same bytes
+    oc, ot = oracle.count_many_parts(host, off, k, 1, host_threads(), 1 << 20)
+    assert np.array_equal(ot, totals)
+    bad = np.nonzero((oc != counts).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} genomes differ, e.g. {bad[:8].tolist()}"
+
+
+@pytest.mark.parametrize("resident", [True, False])
+@pytest.mark.parametrize("rank,world", [(0, 1), (2, 3)])
+def test_configs3_shard_path(torch_dev, oracle, resident, rank, world):
+    """bench.py's configs[3] machinery at total=64, sub-batch 16: the shard plan of
+    rank `rank` of `world` (ids g % world == rank), sub-batches generated on the
+    device, counted resident (one step = every sub-batch) or streamed (each
+    sub-batch generated then timed on its own), every genome of every sub-batch
+    bit-exact vs the oracle and every total analytic."""
+    sys.path.insert(0, ROOT)
+    import bench
+    args = bench.parse_args(["--workload", "configs3", "--total-genomes", "64", "--sub-batch", "16",
+                             "--seq-len", "300000", "--verify", "16"])
+    W = bench.Workload(args, torch_dev, rank, world)
+    ids = [a + i * st for a, st, c in W.plan for i in range(c)]
+    assert ids == list(range(rank, 64, world))
+    assert all(c <= 16 for _, _, c in W.plan) and W.nsb == -(-len(ids) // 16)
+    m = W.measure(7, 2, 1, resident, picks=16, picks_rest=16)
+    assert m["ok"]
+    assert len(m["launch_ms"]) == 2 * W.nsb
+    assert m["el"] > 0
