@@ -181,6 +181,17 @@ int kf_write_kf_rows(const char* path, const char* const* names, int32_t n,
                      const uint32_t* counts, uint64_t nbins, int pseudocount,
                      int raw_cnt, int n_threads);
 
+/* get_chunks, many genomes at once: segment g is rows [seg_row0[g],
+ * seg_row0[g+1]) of counts / names (seg_row0[0] = 0, non-decreasing), written
+ * in row order to paths[g], appended if seg_append && seg_append[g] (a genome
+ * whose windows span several count launches), else truncated.  Rows are
+ * formatted by n_threads host threads, then the segment files are written by
+ * up to n_threads threads (one file each at a time). */
+int kf_write_kf_segments(int32_t n_seg, const char* const* paths, const int32_t* seg_row0,
+                         const uint8_t* seg_append, const char* const* names,
+                         const uint32_t* counts, uint64_t nbins, int pseudocount,
+                         int raw_cnt, int n_threads);
+
 /* ---- get_chunks device pre-pass (replaces seqtk seq -l 0 | awk N-collapse |
  * seqkit seq -g -m, main.py:726-760).  d_seq holds n_rec sorted, disjoint
  * [start, end) byte ranges of record sequences (the bytes between a header's
@@ -189,7 +200,7 @@ int kf_write_kf_rows(const char* path, const char* const* names, int32_t n,
  * N / n / '|' (awk runs before seqkit: gap letters split a run) collapsed to
  * one 'N' -- back to back into d_out (>= len bytes) and its [start, end) into
  * d_out_se[2r], d_out_se[2r+1].  d_scratch: >= ceil(len / 4096) + 1 words.
- * Asynchronous on `stream`. */
+ * len < 2^32 (KF_EINVAL otherwise).  Asynchronous on `stream`. */
 int kf_chunk_compact(const uint8_t* d_bytes, uint64_t len, const uint64_t* d_seq, int32_t n_rec,
                      uint8_t* d_out, uint64_t* d_out_se, uint32_t* d_scratch, uint64_t scratch_words,
                      void* stream);

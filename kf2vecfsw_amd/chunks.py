@@ -8,16 +8,28 @@ The reference shells out per genome to
 then runs one ``get_frequencies -raw_cnt`` (a Jellyfish pair) per window
 (:869-881) and concatenates the rows (:895-915).
 
-Here a genome's bytes go to HBM once; ``kf_chunk_compact`` (csrc/kf_chunks.hip)
-does the linearisation, N-run collapse and gap removal of every record in one
-pass; the host plans the windows from the record lengths (:813-818);
-``kf_chunk_gather`` lays the windows of a batch of genomes out back to back and
-one ``kf_count_batch`` counts them all; ``kf_write_kf_rows`` formats a genome's
-rows with host threads into its one ``.kf`` file.
+Here the genomes are processed in batches of files:
+* the files of a batch are read into one pinned buffer by a thread pool and
+  their header lines indexed (``kf_index_records``);
+* one H2D copy, then ONE ``kf_chunk_compact`` (csrc/kf_chunks.hip) over every
+  record of every genome of the batch: linearisation, N-run collapse and gap
+  removal;
+* ONE device-to-host copy of the processed record bounds per batch; the host
+  plans every genome's windows from them (:813-818, numpy);
+* the windows are gathered into a device buffer (``kf_chunk_gather``) and
+  counted by ``kf_count_batch`` in launches of at most ``max_windows`` windows
+  (the count matrix is 4 x bins bytes per window: 32 KiB at k=7, 8 MiB at k=11);
+* a writer thread formats and writes each launch's rows while the device counts
+  the next launch (``kf_write_kf_segments``: rows formatted by host threads,
+  one file per genome written in parallel, appended when a genome's windows span
+  several launches).
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -46,122 +58,212 @@ def window_name(sample: str, cid: str, s: int) -> str:
     return "{}.part_{}.part_{}_sliding__{}-{}".format(sample, cid, cid, s + 1, s + CHUNK_SZ)
 
 
-def record_regions(data: np.ndarray) -> tuple[np.ndarray, list[str]]:
-    """Sequence regions [start, end) of the FASTA records (the bytes after each
-    header line, up to the next header) and the contig ids (first word of the
-    header, seqtk/seqkit id; a trailing '\\r' of the header line is dropped)."""
-    iv, _ = _index_fasta(data)
-    n = iv.size // 2
-    se = np.empty(2 * n, dtype=np.uint64)
-    ids = []
-    L = data.size
-    for r in range(n):
+def _contig_id(hdr: bytes) -> str:
+    """seqtk/seqkit id: the first word of the header line ('>' and a trailing '\\r' dropped)."""
+    if hdr.endswith(b"\r"):
+        hdr = hdr[:-1]
+    w = hdr.split()
+    return w[0].decode(errors="surrogateescape") if w else ""
+
+
+def records_from_index(data: np.ndarray, iv: np.ndarray, lo: int, hi: int) -> tuple[list[int], list[str]]:
+    """Records of the FASTA bytes data[lo:hi] whose header lines are indexed by iv
+    (kf_index_records pairs, absolute positions): [start, end) of each record's
+    sequence region (the bytes after its header line, up to the next header) as
+    a flat [s0, e0, s1, e1, ...] list, and the contig ids.  kf_index_records
+    merges header lines that follow each other (an empty record, ">a\n>b\n..."),
+    so every interval is split at its newlines: each line is one header."""
+    heads: list[int] = []      # header line starts
+    starts: list[int] = []     # sequence region starts
+    ids: list[str] = []
+    for r in range(iv.size // 2):
         hs, he = int(iv[2 * r]), int(iv[2 * r + 1])
-        se[2 * r] = min(he + 1, L)
-        se[2 * r + 1] = int(iv[2 * r + 2]) if r + 1 < n else L
-        hdr = data[hs + 1: he].tobytes()
-        if hdr.endswith(b"\r"):
-            hdr = hdr[:-1]
-        w = hdr.split()
-        ids.append(w[0].decode(errors="surrogateescape") if w else "")
-    return se, ids
+        pos = hs
+        for line in data[hs: he].tobytes().split(b"\n"):
+            heads.append(pos)
+            starts.append(min(pos + len(line) + 1, hi))
+            ids.append(_contig_id(line[1:]))
+            pos += len(line) + 1
+    ends = heads[1:] + [hi]
+    out = [0] * (2 * len(ids))
+    out[0::2] = starts
+    out[1::2] = ends
+    return out, ids
 
 
-def _index_fasta(data: np.ndarray):
+def record_regions(data: np.ndarray) -> tuple[np.ndarray, list[str]]:
+    """Sequence regions [start, end) of the FASTA records of one genome (the bytes
+    after each header line, up to the next header) and the contig ids (first word
+    of the header, seqtk/seqkit id; a trailing '\\r' of the header line is
+    dropped).  Bytes before the first header belong to no record (seqtk skips them)."""
     from .counter import index_records
-    return index_records(data, N.KF_FMT_FASTA, 0)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    iv, _ = index_records(data, N.KF_FMT_FASTA, 0)
+    se, ids = records_from_index(data, iv, 0, data.size)
+    return np.asarray(se, dtype=np.uint64), ids
 
 
 @dataclass
-class ChunkBatch:
-    """Windows of several genomes laid out back to back on the device."""
-    buf: torch.Tensor                       # uint8, capacity windows x CHUNK_SZ
-    n: int = 0                              # windows so far
-    genomes: list = field(default_factory=list)   # (sample, [row names]) in row order
-
-    @property
-    def capacity(self) -> int:
-        return self.buf.numel() // CHUNK_SZ
+class Genome:
+    """One input file of a batch and its fate (the log lines of main.py:761-885)."""
+    fname: str
+    sample: str
+    rec_lo: int = 0                  # its records in the batch's record table
+    rec_hi: int = 0
+    names: list = field(default_factory=list)
+    starts: np.ndarray | None = None  # window starts in the batch's processed sequence
+    excluded: str | None = None       # "none" (no contig >= 10 kbp) or "few"
+    write: bool = True                # False: a later file has the same sample name
 
 
 class ChunkPipeline:
-    """Device pre-pass + window gather + count + row writer for get_chunks."""
+    """Batched device pre-pass + window plan + count + threaded row writer."""
 
-    def __init__(self, counter, device: torch.device, capacity_windows: int, threads: int):
+    def __init__(self, counter, device: torch.device, max_windows: int, threads: int,
+                 pseudocount: bool = False):
         self.counter = counter
-        self.device = device
+        self.device = torch.device(device)
         self.threads = max(1, int(threads))
-        self.batch = ChunkBatch(torch.empty(max(1, capacity_windows) * CHUNK_SZ, dtype=torch.uint8, device=device))
+        self.max_windows = max(1, int(max_windows))
+        self.pseudocount = bool(pseudocount)
+        self.writer = ThreadPoolExecutor(max_workers=1)   # launches are written in order
+        self.pending = []
+        self._wbuf = None
 
-    def windows_of(self, data: bytes, sample: str) -> tuple[list[str], np.ndarray, torch.Tensor]:
-        """(row names, window starts in the processed sequence, processed sequence
-        on the device) of one genome; no window if no contig reaches 10 kbp."""
-        host = np.frombuffer(data, dtype=np.uint8)
-        se, ids = record_regions(host)
-        if se.size == 0:
-            return [], np.zeros(0, np.uint64), None
+    # ------------------------------------------------------------ pre-pass
+    def prepare(self, hb, genomes: list[Genome]) -> torch.Tensor:
+        """Compact every record of the batch on the device and plan the windows of
+        every genome (one device-to-host copy).  Fills genomes[i].names/starts/
+        excluded; returns the processed sequence buffer (device)."""
+        data = hb.data.numpy()
+        rec_se: list[int] = []
+        rec_ids: list[str] = []
+        ex = hb.excl
+        # the batch's header intervals, per genome (sorted, genome by genome)
+        bounds = np.searchsorted(ex[0::2], hb.off) if ex.size else np.zeros(hb.off.size, np.int64)
+        for g, gm in enumerate(genomes):
+            lo, hi = int(hb.off[g]), int(hb.off[g + 1])
+            iv = ex[2 * int(bounds[g]): 2 * int(bounds[g + 1])]
+            se, ids = records_from_index(data, iv, lo, hi)
+            gm.rec_lo = len(rec_ids)
+            rec_se += se
+            rec_ids += ids
+            gm.rec_hi = len(rec_ids)
+        n_rec = len(rec_ids)
         dev = self.device
-        s = torch.cuda.current_stream(dev).cuda_stream
-        d_bytes = torch.from_numpy(host.copy()).to(dev, non_blocking=False)
-        d_seq = torch.from_numpy(se.view(np.int64)).to(dev)
-        d_out = torch.empty(max(host.size, 16), dtype=torch.uint8, device=dev)
-        d_se = torch.empty(se.size, dtype=torch.int64, device=dev)
-        nwords = (host.size + 4095) // 4096 + 1
-        scratch = torch.empty(nwords, dtype=torch.int32, device=dev)
-        N.check(N.lib().kf_chunk_compact(d_bytes.data_ptr(), host.size, d_seq.data_ptr(), se.size // 2,
-                                         d_out.data_ptr(), d_se.data_ptr(), scratch.data_ptr(), nwords, s),
-                "kf_chunk_compact")
-        out_se = d_se.cpu().numpy().view(np.uint64)          # (synchronises the stream)
-        names, starts = [], []
-        for r, cid in enumerate(ids):
-            a, b = int(out_se[2 * r]), int(out_se[2 * r + 1])
-            L = b - a
-            if L < CHUNK_SZ:                                   # seqkit seq -m 10000 (main.py:753)
-                continue
-            n, step = window_plan(L)
-            for i in range(n):
-                names.append(window_name(sample, cid, i * step))
-                starts.append(a + i * step)
-        return names, np.asarray(starts, dtype=np.uint64), d_out
+        stream = torch.cuda.current_stream(dev)
+        total = int(hb.off[-1])
+        d_bytes = hb.data.to(dev, non_blocking=True)
+        d_out = torch.empty(max(total, 16) + 16, dtype=torch.uint8, device=dev)
+        if n_rec:
+            host_se = torch.from_numpy(np.asarray(rec_se, dtype=np.int64))
+            if hb.data.is_pinned():
+                host_se = host_se.pin_memory()
+            d_se_in = host_se.to(dev, non_blocking=True)
+            d_se = torch.empty(2 * n_rec, dtype=torch.int64, device=dev)
+            nwords = (total + 4095) // 4096 + 1
+            scratch = torch.empty(nwords, dtype=torch.int32, device=dev)
+            N.check(N.lib().kf_chunk_compact(d_bytes.data_ptr(), total, d_se_in.data_ptr(), n_rec, d_out.data_ptr(),
+                                             d_se.data_ptr(), scratch.data_ptr(), nwords, stream.cuda_stream),
+                    "kf_chunk_compact")
+            out_se = d_se.cpu().numpy().view(np.uint64)      # the batch's one synchronising copy
+        else:
+            out_se = np.zeros(0, np.uint64)
+        for gm in genomes:
+            names, starts = [], []
+            for r in range(gm.rec_lo, gm.rec_hi):
+                a, b = int(out_se[2 * r]), int(out_se[2 * r + 1])
+                L = b - a
+                if L < CHUNK_SZ:                                   # seqkit seq -m 10000 (main.py:753)
+                    continue
+                n, step = window_plan(L)
+                cid = rec_ids[r]
+                pos = np.arange(n, dtype=np.int64) * step
+                starts.append(a + pos)
+                pre = "{}.part_{}.part_{}_sliding__".format(gm.sample, cid, cid)
+                names += [pre + "{}-{}".format(p + 1, p + CHUNK_SZ) for p in pos.tolist()]
+            if not starts:
+                gm.excluded = "none"                               # main.py:761-778
+            elif len(names) < CHUNK_CNT_THR:
+                gm.excluded = "few"                                # main.py:845-860
+            gm.names = names
+            gm.starts = np.concatenate(starts) if starts else np.zeros(0, np.int64)
+        # the reference writes genome by genome, so a later file with the same
+        # sample name replaces an earlier one's .kf: inside a batch, only the last
+        # written one is counted (across batches the in-order writer does it)
+        kept = set()
+        for gm in reversed(genomes):
+            if gm.excluded is None:
+                gm.write = gm.sample not in kept
+                kept.add(gm.sample)
+        return d_out
 
-    def add(self, sample: str, names: list[str], starts: np.ndarray, d_seq: torch.Tensor, flush) -> None:
-        """Gather a genome's windows into the batch (flushing it first if full)."""
-        if self.batch.n + len(names) > self.batch.capacity:
-            flush()
-            if len(names) > self.batch.capacity:   # one genome larger than the batch: grow it
-                self.batch = ChunkBatch(torch.empty(len(names) * CHUNK_SZ, dtype=torch.uint8, device=self.device))
-        b = self.batch
-        d_src = torch.from_numpy(starts.view(np.int64)).to(self.device)
-        dst = b.buf[b.n * CHUNK_SZ:]
-        N.check(N.lib().kf_chunk_gather(d_seq.data_ptr(), d_src.data_ptr(), len(names), CHUNK_SZ, dst.data_ptr(),
-                                        torch.cuda.current_stream(self.device).cuda_stream), "kf_chunk_gather")
-        b.n += len(names)
-        b.genomes.append((sample, names))
+    # ------------------------------------------------------------ count + write
+    def count_and_write(self, d_seq: torch.Tensor, genomes: list[Genome], output_dir: str) -> list:
+        """Gather, count and (asynchronously) write the windows of the batch's
+        kept genomes, at most max_windows per count launch.  Returns the futures
+        of the batch's writes."""
+        work = [g for g in genomes if g.excluded is None and g.write]
+        futs = []
+        if not work:
+            return futs
+        dev = self.device
+        # flat window list of the batch, with its genome boundaries
+        starts = np.concatenate([g.starts for g in work]).astype(np.int64)
+        row0 = np.cumsum([0] + [len(g.names) for g in work])
+        total = int(row0[-1])
+        d_starts = torch.from_numpy(starts).pin_memory().to(dev, non_blocking=True)
+        stream = torch.cuda.current_stream(dev)
+        for w0 in range(0, total, self.max_windows):
+            w1 = min(total, w0 + self.max_windows)
+            nw = w1 - w0
+            if self._wbuf is None or self._wbuf.numel() < nw * CHUNK_SZ:
+                self._wbuf = torch.empty(nw * CHUNK_SZ, dtype=torch.uint8, device=dev)
+            N.check(N.lib().kf_chunk_gather(d_seq.data_ptr(), d_starts[w0:].data_ptr(), nw, CHUNK_SZ,
+                                            self._wbuf.data_ptr(), stream.cuda_stream), "kf_chunk_gather")
+            from .counter import DeviceBatch
+            off = torch.arange(0, (nw + 1) * CHUNK_SZ, CHUNK_SZ, dtype=torch.int64, device=dev)
+            db = DeviceBatch(self._wbuf, off, torch.zeros(2, dtype=torch.int64, device=dev), nw, 0)
+            counts, _ = self.counter.count(db)
+            host = torch.empty(counts.shape, dtype=counts.dtype, pin_memory=True)
+            host.copy_(counts, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            # the segments of this launch: each genome's rows inside [w0, w1)
+            segs = []
+            for gi, g in enumerate(work):
+                a, b = max(int(row0[gi]), w0), min(int(row0[gi + 1]), w1)
+                if a >= b:
+                    continue
+                segs.append((os.path.join(output_dir, "{}.kf".format(g.sample)), a - w0, b - w0,
+                             g.names[a - int(row0[gi]): b - int(row0[gi])], a > int(row0[gi])))
+            if len(self.pending) >= 2:      # at most two launches queued for the writer
+                self.pending.pop(0).result()
+            futs.append(self.writer.submit(self._write, ev, host, segs))
+            self.pending.append(futs[-1])
+            del counts
+        return futs
 
-    def count_and_write(self, output_dir: str, pseudocount: bool, written) -> None:
-        """Count every window of the batch in one kf_count_batch and write each
-        genome's rows into <output_dir>/<sample>.kf (raw counts, main.py:869-915)."""
-        import ctypes
-        import os
-
-        from .counter import DeviceBatch, counts_to_numpy
-        b = self.batch
-        if b.n == 0:
+    def _write(self, ev, host: torch.Tensor, segs) -> None:
+        """Format + write one launch's rows (segments are consecutive row ranges)."""
+        ev.synchronize()
+        if not segs:
             return
-        dev = self.device
-        off = torch.arange(0, (b.n + 1) * CHUNK_SZ, CHUNK_SZ, dtype=torch.int64, device=dev)
-        db = DeviceBatch(b.buf, off, torch.zeros(2, dtype=torch.int64, device=dev), b.n, 0)
-        counts, _ = self.counter.count(db)
-        c = counts_to_numpy(counts)
-        row = 0
-        for sample, names in b.genomes:
-            enc = [n.encode(errors="surrogateescape") for n in names]
-            arr = (ctypes.c_char_p * len(enc))(*enc)
-            rows = np.ascontiguousarray(c[row: row + len(names)])
-            N.check(N.lib().kf_write_kf_rows(os.fsencode(os.path.join(output_dir, "{}.kf".format(sample))), arr,
-                                             len(enc), rows.ctypes.data, rows.shape[1], int(bool(pseudocount)), 1,
-                                             self.threads), "kf_write_kf_rows")
-            row += len(names)
-            written(sample)
-        b.n = 0
-        b.genomes = []
+        rows = host.numpy().view(np.uint32)
+        paths = (ctypes.c_char_p * len(segs))(*[os.fsencode(s[0]) for s in segs])
+        row0 = np.asarray([0] + [s[2] for s in segs], dtype=np.int32)
+        app = np.asarray([1 if s[4] else 0 for s in segs], dtype=np.uint8)
+        enc = [n.encode(errors="surrogateescape") for s in segs for n in s[3]]
+        arr = (ctypes.c_char_p * len(enc))(*enc)
+        N.check(N.lib().kf_write_kf_segments(len(segs), paths, row0.ctypes.data, app.ctypes.data, arr,
+                                             rows.ctypes.data, rows.shape[1], int(self.pseudocount), 1,
+                                             self.threads), "kf_write_kf_segments")
+
+    def drain(self) -> None:
+        """Wait for every queued write."""
+        while self.pending:
+            self.pending.pop(0).result()
+
+    def close(self) -> None:
+        self.drain()
+        self.writer.shutdown()

@@ -198,9 +198,12 @@ extern "C" int kf_chunk_compact(const uint8_t* d_bytes, uint64_t len, const uint
     if (n_rec < 0) return kf_fail(KF_EINVAL, "n_rec < 0");
     if (n_rec == 0) return KF_OK;
     if (!d_bytes || !d_seq || !d_out || !d_out_se || !d_scratch) return kf_fail(KF_EINVAL, "null device pointer");
+    // block counts, their scan and the record bounds are 32-bit: the processed
+    // sequence of one call must stay below 4 GiB
+    if (len >= (1ull << 32)) return kf_fail(KF_EINVAL, "input of %llu bytes: at most 4 GiB - 1 per call",
+                                            (unsigned long long)len);
     const uint64_t nb = (len + kCSpan - 1) / kCSpan;
     if (scratch_words < nb + 1) return kf_fail(KF_ERANGE, "scratch needs %llu words", (unsigned long long)(nb + 1));
-    if (nb >= 0xFFFFFFFFull) return kf_fail(KF_EINVAL, "input too large");
     hipStream_t s = (hipStream_t)stream;
     if (nb) {
         hipLaunchKernelGGL(chunk_count_kernel, dim3((uint32_t)nb), dim3(kCBlock), 0, s, d_bytes, len, d_seq, n_rec,

@@ -241,6 +241,30 @@ inline char* fmt_u64(uint64_t v, char* p) {
     return r.ptr;
 }
 
+// Small counts are most of a row (a 10 kbp get_chunks window has 8,192 columns
+// at k=7, nearly all 0-3): their text comes from a table built once.
+//   kSmallInt[c] = "c", kSmallHalf[c] = "c.5" (pseudocount), kSmallF[c] = "c.0"
+constexpr uint32_t kSmall = 1024;
+struct SmallText {
+    char txt[3][kSmall][8];
+    uint8_t len[3][kSmall];
+    SmallText() {
+        for (uint32_t c = 0; c < kSmall; ++c) {
+            for (int m = 0; m < 3; ++m) {
+                char* p = txt[m][c];
+                char* e = fmt_u64(c, p);
+                if (m == 1) { *e++ = '.'; *e++ = '5'; }
+                if (m == 2) { *e++ = '.'; *e++ = '0'; }
+                len[m][c] = (uint8_t)(e - p);
+            }
+        }
+    }
+};
+const SmallText& small_text() {
+    static const SmallText t;
+    return t;
+}
+
 uint64_t kf_line_cap(size_t name_len, uint64_t nbins) { return name_len + 2 + nbins * 26; }
 
 // main.py:327-357
@@ -263,13 +287,27 @@ uint64_t format_line(const char* name, const uint32_t* c, uint64_t nb, int pseud
     // NaN, which fillna(0) fills with the int 0).  Pinned by
     // tests/golden/ref_postproc (dense_k3_raw, empty_k7_raw).
     const bool int_text = raw && !pseudo && (all_present || sum == 0.0);
-    for (uint64_t i = 0; i < nb; ++i) {
-        if (i) *p++ = ',';
-        if (int_text) {
-            p = fmt_u64(c[i], p);
-        } else {
-            double v = (double)c[i] + (pseudo ? 0.5 : 0.0);
-            if (!raw) v = v / sum;
+    if (raw) {
+        // raw counts: "c" (integer text), "c.5" (pseudocount) or "c.0" -- what
+        // repr prints for an integral float64 below 1e16 (and c + 0.5 < 2^33)
+        const SmallText& T = small_text();
+        const int m = int_text ? 0 : (pseudo ? 1 : 2);
+        for (uint64_t i = 0; i < nb; ++i) {
+            if (i) *p++ = ',';
+            const uint32_t v = c[i];
+            if (v < kSmall) {
+                memcpy(p, T.txt[m][v], 8);   // the row buffer has >= 26 B per column
+                p += T.len[m][v];
+            } else {
+                p = fmt_u64(v, p);
+                if (m == 1) { *p++ = '.'; *p++ = '5'; }
+                if (m == 2) { *p++ = '.'; *p++ = '0'; }
+            }
+        }
+    } else {
+        for (uint64_t i = 0; i < nb; ++i) {
+            if (i) *p++ = ',';
+            const double v = ((double)c[i] + (pseudo ? 0.5 : 0.0)) / sum;
             p = fmt_repr(v, p);
         }
     }
@@ -330,32 +368,72 @@ extern "C" int kf_write_kf_files(const char* dir, const char* const* names, int3
     return KF_OK;
 }
 
-extern "C" int kf_write_kf_rows(const char* path, const char* const* names, int32_t n, const uint32_t* counts,
-                                uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
-    if (!path || (!names && n) || (!counts && n) || n < 0) return kf_fail(KF_EINVAL, "null argument");
+// Row-granular parallel formatting of every row of every segment, then one
+// sequential write per segment file (segments in parallel, rows in order).
+extern "C" int kf_write_kf_segments(int32_t n_seg, const char* const* paths, const int32_t* seg_row0,
+                                    const uint8_t* seg_append, const char* const* names, const uint32_t* counts,
+                                    uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
+    if (n_seg < 0 || (n_seg && (!paths || !seg_row0))) return kf_fail(KF_EINVAL, "null argument");
+    if (n_seg == 0) return KF_OK;
+    const int32_t n = seg_row0[n_seg];
+    if (seg_row0[0] != 0 || n < 0) return kf_fail(KF_EINVAL, "seg_row0 must start at 0");
+    for (int32_t g = 0; g < n_seg; ++g)
+        if (seg_row0[g + 1] < seg_row0[g]) return kf_fail(KF_EINVAL, "seg_row0 must be non-decreasing");
+    if (n && (!names || !counts)) return kf_fail(KF_EINVAL, "null argument");
     if (n_threads < 1) n_threads = 1;
-    n_threads = std::min<int>(n_threads, std::max<int32_t>(n, 1));
     std::vector<std::vector<char>> rows((size_t)n);
-    std::vector<uint64_t> len((size_t)n, 0);
     std::atomic<int32_t> next{0};
-    auto work = [&]() {
+    auto fmt = [&]() {
+        std::vector<char> buf;
         for (;;) {
             const int32_t i = next.fetch_add(1);
             if (i >= n) break;
-            rows[i].resize(kf_line_cap(strlen(names[i]), nbins));
-            len[i] = format_line(names[i], counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt, rows[i].data());
+            buf.resize(kf_line_cap(strlen(names[i]), nbins));
+            const uint64_t w = format_line(names[i], counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt,
+                                           buf.data());
+            rows[i].assign(buf.data(), buf.data() + w);
         }
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < n_threads; ++t) th.emplace_back(work);
-    work();
-    for (auto& t : th) t.join();
-    FILE* f = fopen(path, "wb");
-    bool ok = f != nullptr;
-    for (int32_t i = 0; ok && i < n; ++i) ok = fwrite(rows[i].data(), 1, len[i], f) == len[i];
-    if (f) ok = (fclose(f) == 0) && ok;
-    if (!ok) return kf_fail(KF_EINVAL, "cannot write %s", path);
+    std::atomic<int32_t> next_seg{0};
+    std::atomic<int> err{0};
+    std::string errmsg;
+    std::mutex mu;
+    auto wr = [&]() {
+        for (;;) {
+            const int32_t g = next_seg.fetch_add(1);
+            if (g >= n_seg || err.load()) break;
+            FILE* f = fopen(paths[g], (seg_append && seg_append[g]) ? "ab" : "wb");
+            bool ok = f != nullptr;
+            for (int32_t i = seg_row0[g]; ok && i < seg_row0[g + 1]; ++i)
+                ok = fwrite(rows[i].data(), 1, rows[i].size(), f) == rows[i].size();
+            if (f) ok = (fclose(f) == 0) && ok;
+            if (!ok) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!err.exchange(1)) errmsg = std::string("cannot write ") + paths[g];
+            }
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 1; t < std::min<int>(n_threads, std::max<int32_t>(n, 1)); ++t) th.emplace_back(fmt);
+        fmt();
+        for (auto& t : th) t.join();
+    }
+    {
+        std::vector<std::thread> th;
+        for (int t = 1; t < std::min<int>(n_threads, n_seg); ++t) th.emplace_back(wr);
+        wr();
+        for (auto& t : th) t.join();
+    }
+    if (err.load()) return kf_fail(KF_EINVAL, "%s", errmsg.c_str());
     return KF_OK;
+}
+
+extern "C" int kf_write_kf_rows(const char* path, const char* const* names, int32_t n, const uint32_t* counts,
+                                uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
+    if (!path || (!names && n) || (!counts && n) || n < 0) return kf_fail(KF_EINVAL, "null argument");
+    const int32_t row0[2] = {0, n};
+    return kf_write_kf_segments(1, &path, row0, nullptr, names, counts, nbins, pseudocount, raw_cnt, n_threads);
 }
 
 // ------------------------------------------------------------------ synthetic layout

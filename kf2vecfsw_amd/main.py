@@ -16,6 +16,7 @@ import fnmatch
 import multiprocessing as mp
 import os
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -134,14 +135,17 @@ def _spawn_shards(argv: list[str], world: int) -> int:
     return max(abs(p.wait()) for p in procs)
 
 
-def visible_gpus() -> int:
+def visible_gpus() -> int | None:
     """GPUs this process may use, counted without initialising HIP (the -gpus
-    parent forks children and must never touch the GPU itself): the first of
-    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES that is set,
-    capped by the GPU nodes of the KFD topology (nodes with SIMDs)."""
+    parent forks children and must never touch the GPU itself): the GPU nodes of
+    the KFD topology (nodes with SIMDs), capped by every one of
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES that is set
+    (HIP applies its mask on top of ROCR's, so the smallest wins).  None when the
+    topology is unreadable and no mask is set: unknown."""
     topo = "/sys/class/kfd/kfd/topology/nodes"
-    n_kfd = 0
+    n_kfd = None
     try:
+        n_kfd = 0
         for d in os.listdir(topo):
             try:
                 props = open(os.path.join(topo, d, "properties")).read().split("\n")
@@ -150,14 +154,13 @@ def visible_gpus() -> int:
             if any(ln.startswith("simd_count") and ln.split()[-1] != "0" for ln in props):
                 n_kfd += 1
     except OSError:
-        pass
+        n_kfd = None
     n = n_kfd
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
         if v is not None:
             ids = [x for x in v.split(",") if x.strip() != ""]
-            n = min(n, len(ids)) if n_kfd else len(ids)
-            break
+            n = len(ids) if n is None else min(n, len(ids))
     return n
 
 
@@ -174,8 +177,10 @@ def get_frequencies(args) -> None:
         world = args.gpus
         avail = visible_gpus()
         if world <= 0:
+            if avail is None:
+                raise ValueError("-gpus 0: cannot count the visible GPUs (no KFD topology, no *_VISIBLE_DEVICES)")
             world = max(1, avail)
-        elif not os.environ.get("KF_SHARD_DEVICE") and world > avail:
+        elif not os.environ.get("KF_SHARD_DEVICE") and avail is not None and world > avail:
             raise ValueError("-gpus {}: only {} GPU(s) visible".format(world, avail))
         if world > 1:
             print("\n==> Starting k-mer counting for {}\n".format(args.input_dir))
@@ -466,17 +471,22 @@ def _hms(seconds: float) -> tuple[int, int, int]:
 
 
 def get_chunks(args) -> None:
-    """kf2vec/main.py:654-929: each genome's records are linearised, N-collapsed
-    and gap-filtered on the device (kf_chunk_compact), its 10 kbp windows are
-    gathered into a device batch with other genomes' windows, and one
-    kf_count_batch counts the batch -- instead of seqtk + awk + seqkit per genome
-    and one Jellyfish pair per window."""
+    """kf2vec/main.py:654-929 in batches of genome files: each batch is read and
+    header-indexed by host threads, linearised / N-collapsed / gap-filtered on the
+    device in one pass (kf_chunk_compact), its windows planned from one copy of
+    the record bounds, gathered and counted in launches of bounded size, and
+    written by a writer thread while the device counts the next launch -- instead
+    of seqtk + awk + seqkit per genome and one Jellyfish pair per window.
+
+    Log lines: the reference's per-genome lines ("Start processing", "Done chunk
+    processing" or "Excluded ...", "Done computing k-mer frequences") come in its
+    order, genome by genome, once the genome's rows are written (so a genome's
+    three lines are logged together, after its batch is counted)."""
     import logging
     import time
 
-    import torch
     from . import chunks as CH
-    from .counter import KmerCounter
+    from .counter import KmerCounter, pack_files
 
     since = time.time()
     if not os.path.exists(args.input_dir):
@@ -502,33 +512,60 @@ def get_chunks(args) -> None:
     if args.k not in supported_k:
         raise ValueError("k={} has no vocabulary: supported k are {}..{}".format(
             args.k, supported_k.start, supported_k.stop - 1))
+    import torch
     device = torch.device(getattr(args, "device", None) or "cuda")
     counter = KmerCounter(args.k, device)
     budget = int(float(getattr(args, "batch_gb", 1.0) or 1.0) * (1 << 30))
-    pipe = CH.ChunkPipeline(counter, device, max(1, budget // CH.CHUNK_SZ), args.p)
-    fname_of = dict(zip(samples_names, files_names))
+    # windows per count launch: the window bytes AND the count matrix (4 x bins
+    # per window, 8 MiB at k=11) within the budget
+    max_windows = max(1, min(budget // CH.CHUNK_SZ, budget // (4 * counter.nbins)))
+    pipe = CH.ChunkPipeline(counter, device, max_windows, args.p, args.pseudocount)
+    paths = [os.path.join(args.input_dir, f) for f in files_names]
+    # input batches of files (the processed sequence of a batch must stay below
+    # 4 GiB: kf_chunk_compact's offsets)
+    batches = _batches(paths, min(budget, 3 << 30))
+    threads = max(1, int(args.p))
+    files_pool = ThreadPoolExecutor(max_workers=threads)
+    reader = ThreadPoolExecutor(max_workers=1)
 
-    def written(sample):
-        stamp("\n==> Done computing k-mer frequences for {}.".format(fname_of.get(sample, sample)))
+    def read(idx):
+        return pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], fmt=N.KF_FMT_FASTA,
+                          pool=files_pool)
 
-    def flush():
-        pipe.count_and_write(args.output_dir, args.pseudocount, written)
+    def report(genomes):
+        for gm in genomes:
+            log.info("\n==> Start processing. Sample: {}".format(gm.fname))
+            if gm.excluded == "none":                                    # main.py:761-778
+                stamp("\n==> Excluded {}. No contigs above threshold length.".format(gm.fname))
+            elif gm.excluded == "few":                                   # main.py:845-860
+                stamp("\n==> Excluded {}. {} chunks is too low. {} is required.".format(
+                    gm.fname, len(gm.names), CH.CHUNK_CNT_THR))
+            else:
+                stamp("\n==> Done chunk processing for {}.".format(gm.fname))
+                stamp("\n==> Done computing k-mer frequences for {}.".format(gm.fname))
 
-    for fname, sample in zip(files_names, samples_names):
-        log.info("\n==> Start processing. Sample: {}".format(fname))
-        with open(os.path.join(args.input_dir, fname), "rb") as f:
-            data = f.read()
-        names, starts, d_seq = pipe.windows_of(data, sample)
-        if not names:   # no contig of >= 10 kbp after N-collapse / gap removal (main.py:761-778)
-            stamp("\n==> Excluded {}. No contigs above threshold length.".format(fname))
-            continue
-        if len(names) < CH.CHUNK_CNT_THR:                                  # main.py:845-860
-            stamp("\n==> Excluded {}. {} chunks is too low. {} is required.".format(
-                fname, len(names), CH.CHUNK_CNT_THR))
-            continue
-        stamp("\n==> Done chunk processing for {}.".format(fname))
-        pipe.add(sample, names, starts, d_seq, flush)
-    flush()
+    nxt = reader.submit(read, batches[0]) if batches else None
+    prev = None   # (genomes, write futures) of the previous batch, logged once written
+    for bi, idx in enumerate(batches):
+        hb = nxt.result()
+        if bi + 1 < len(batches):
+            nxt = reader.submit(read, batches[bi + 1])
+        genomes = [CH.Genome(files_names[i], samples_names[i]) for i in idx]
+        d_seq = pipe.prepare(hb, genomes)
+        futs = pipe.count_and_write(d_seq, genomes, args.output_dir)
+        del hb, d_seq
+        if prev is not None:
+            for f in prev[1]:
+                f.result()
+            report(prev[0])
+        prev = (genomes, futs)
+    if prev is not None:
+        for f in prev[1]:
+            f.result()
+        report(prev[0])
+    pipe.close()
+    reader.shutdown()
+    files_pool.shutdown()
     stamp("\n==> Done getting chunks.")
 
 

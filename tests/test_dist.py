@@ -163,3 +163,12 @@ def test_cli_gpus_validation(monkeypatch, tmp_path):
     monkeypatch.setenv("WORLD_SIZE", "1")
     with pytest.raises(ValueError, match="visible"):
         M.get_frequencies(a)
+    # HIP's mask applies on top of ROCR's: the smallest of the set masks wins
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert M.visible_gpus() <= 1
+    # no mask and no readable KFD topology: unknown, not 0 (no check then)
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    if not os.path.isdir("/sys/class/kfd/kfd/topology/nodes"):
+        assert M.visible_gpus() is None

@@ -629,6 +629,8 @@ def _chunk_genome(rng, n_contigs):
         body = gen.wrap(seq, int(rng.choice([60, 70, 80, 1000])), crlf=bool(rng.random() < 0.3))
         if rng.random() < 0.2:
             body = body.replace(b"\n", b"\n\n", 3)
+        if rng.random() < 0.2:
+            out.append(b">empty%d\n" % c)            # an empty record: its header merges with the next
         out.append(b">ctg%d some description\n" % c + body)
     return b"".join(out)
 
@@ -638,15 +640,25 @@ def test_chunk_compact_matches_oracle(torch_dev, oracle):
     oracle's restatement of seqtk seq -l 0 | awk gsub | seqkit seq -g, record by
     record, and every window of get_chunks' plan counts like the oracle."""
     from kf2vecfsw_amd import chunks as CH
+    from kf2vecfsw_amd import counter as C
+    from kf2vecfsw_amd import _native as N
     rng = np.random.default_rng(4040)
-    for t in range(6):
-        data = _chunk_genome(rng, int(rng.integers(1, 12)))
-        names, starts, d_seq = CH.ChunkPipeline(counter(7, torch_dev), torch_dev, 16, 2).windows_of(data, "s")
-        exp = oracle.chunk_windows(data, "s")
-        assert names == [n for n, _ in exp]
-        got = d_seq.cpu().numpy()
-        for st, (_, w) in zip(starts, exp):
-            assert got[int(st): int(st) + 10000].tobytes() == w
+    datas = [_chunk_genome(rng, int(rng.integers(1, 12))) for _ in range(6)]
+    datas += [b">a\n>b x\n" + gen.wrap(gen.random_seq(rng, 23000), 60) + b">c\n>d\n>e\n" +
+              gen.wrap(gen.random_seq(rng, 12000), 80)]                  # empty records (merged headers)
+    pipe = CH.ChunkPipeline(counter(7, torch_dev), torch_dev, 16, 2)
+    # one batch of every genome (one compaction over all their records) and one genome per batch
+    for group in (list(range(len(datas))), [3], [len(datas) - 1]):
+        hb = C.pack_genomes([datas[i] for i in group], [f"s{i}" for i in group], fmt=N.KF_FMT_FASTA)
+        genomes = [CH.Genome(f"s{i}.fna", f"s{i}") for i in group]
+        got = pipe.prepare(hb, genomes).cpu().numpy()
+        for i, gm in zip(group, genomes):
+            exp = oracle.chunk_windows(datas[i], f"s{i}")
+            assert gm.names == [n for n, _ in exp], i
+            for st, (_, w) in zip(gm.starts, exp):
+                assert got[int(st): int(st) + 10000].tobytes() == w
+            assert gm.excluded == (None if len(exp) >= 5 else ("none" if not exp else "few"))
+    pipe.close()
 
 
 def test_cli_get_chunks_multicontig_vs_oracle(torch_dev, oracle, tmp_path):
@@ -704,3 +716,40 @@ def test_features_handoff_equals_kf_text_round_trip(torch_dev, toy, tmp_path):
                 dflt = pd.read_csv(f, index_col=0, header=None, sep=",").values.astype(np.float64)[0]
                 assert np.all(np.abs(dflt[ok] - X1[i][ok]) <= 1e-12 * np.abs(X1[i][ok])), (name, pseudo, raw)
     torch.cuda.synchronize()
+
+
+def test_cli_get_chunks_large_k_bounded_launches(torch_dev, oracle, tmp_path):
+    """get_chunks at k=10 (524,800 columns, 2 MiB of counts per window) with a
+    budget that allows 5 windows per count launch: each genome's windows span
+    several launches (rows appended in order), every row == the oracle's raw
+    counts, and the launch size is bounded by the count matrix."""
+    from kf2vecfsw_amd import chunks as CH
+    from kf2vecfsw_amd import main as M
+    rng = np.random.default_rng(6060)
+    inp, out = tmp_path / "in", tmp_path / "out"
+    inp.mkdir()
+    out.mkdir()
+    genomes = {f"h{i}": _chunk_genome(rng, 3) + b">tail\n" + gen.wrap(gen.random_seq(rng, 61000), 80)
+               for i in range(2)}
+    for name, b in genomes.items():
+        (inp / f"{name}.fna").write_bytes(b)
+    budget = int(0.01 * (1 << 30))
+    assert max(1, min(budget // CH.CHUNK_SZ, budget // (4 * 524800))) == 5
+    seen = []
+    orig = CH.ChunkPipeline.count_and_write
+
+    def spy(self, d_seq, gms, output_dir):
+        seen.append(self.max_windows)
+        return orig(self, d_seq, gms, output_dir)
+
+    CH.ChunkPipeline.count_and_write = spy
+    try:
+        M.main(["get_chunks", "-input_dir", str(inp), "-output_dir", str(out), "-k", "10", "-batch_gb", "0.01"])
+    finally:
+        CH.ChunkPipeline.count_and_write = orig
+    assert seen and all(m == 5 for m in seen)
+    for name, b in genomes.items():
+        wins = oracle.chunk_windows(b, name)
+        assert len(wins) > 5
+        exp = "".join(oracle.kf_line(n, oracle.count(b">w\n" + w + b"\n", 10)[0], raw_cnt=True) for n, w in wins)
+        assert (out / f"{name}.kf").read_text() == exp, name

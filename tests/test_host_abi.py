@@ -158,6 +158,13 @@ def test_chunk_record_regions(native):
     assert ids == ["c1", "c2", "", "c4"]
     regs = [data[int(se[2 * i]): int(se[2 * i + 1])].tobytes() for i in range(len(ids))]
     assert regs == [b"ACGT\nAC\n", b"GG\n", b"\n", b""]
+    # consecutive header lines (empty records) are merged by kf_index_records: each
+    # line is still its own record, so b's windows are named after b
+    data = np.frombuffer(b">a\n>b y\r\n>c\nACGT\n>d\n>e", np.uint8)
+    se, ids = CH.record_regions(data)
+    assert ids == ["a", "b", "c", "d", "e"]
+    regs = [data[int(se[2 * i]): int(se[2 * i + 1])].tobytes() for i in range(len(ids))]
+    assert regs == [b"", b"", b"ACGT\n", b"", b""]
 
 
 def test_get_kmers_matrix_matches_reference_restatement(native, oracle):

@@ -12,7 +12,9 @@ Every output row of the toy run is checked against the reference's committed
 chunk files (358 rows).
 """
 import argparse
+import contextlib
 import gzip
+import io
 import json
 import os
 import shutil
@@ -30,7 +32,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--genomes", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--dir", default="/tmp/kf_chunks_bench")
+    ap.add_argument("--dir", default="/dev/shm/kf_chunks_bench" if os.access("/dev/shm", os.W_OK)
+                    else "/tmp/kf_chunks_bench")
+    ap.add_argument("--threads", type=int, default=16)
     args = ap.parse_args()
     from kf2vecfsw_amd import main as M
     from test_gpu_parity import _bacterial_like
@@ -56,10 +60,12 @@ def main():
             shutil.rmtree(out, ignore_errors=True)
             os.makedirs(out)
             t0 = time.perf_counter()
-            M.main(["get_chunks", "-input_dir", inp, "-output_dir", out, "-k", "7", "-p", "16"])
+            with contextlib.redirect_stdout(io.StringIO()):
+                M.main(["get_chunks", "-input_dir", inp, "-output_dir", out, "-k", "7", "-p", str(args.threads)])
             if r:   # the first run warms the runtime and the page cache
                 walls.append(time.perf_counter() - t0)
         rows = sum(open(os.path.join(out, f)).read().count("\n") for f in os.listdir(out) if f.endswith(".kf"))
+        kfb = sum(os.path.getsize(os.path.join(out, f)) for f in os.listdir(out) if f.endswith(".kf"))
         ok = None
         if name == "toy":
             ok = True
@@ -71,7 +77,9 @@ def main():
         res[name] = {"windows": rows, "wall_s_median": round(w, 4), "windows_per_s": round(rows / w, 1),
                      "ms_per_window": round(w / rows * 1e3, 4),
                      "vs_reference_64ms_per_chunk": round(0.064 / (w / rows), 1),
+                     "kf_bytes": kfb, "kf_GBps": round(kfb / w / 1e9, 2), "walls": [round(x, 4) for x in walls],
                      "reference_rows_match": ok}
+    shutil.rmtree(args.dir, ignore_errors=True)
     print(json.dumps(res, indent=1))
 
 
