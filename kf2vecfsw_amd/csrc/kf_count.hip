@@ -5,7 +5,7 @@
 // kf2vec/main.py:309-328: `jellyfish count -C` + `jellyfish dump -c` + the
 // pandas merge onto the sorted vocabulary).  k >= 9 is kf_bucket.hip.
 //
-// Work decomposition, shared by both kernels:
+// Work decomposition:
 //   * the batch [goff[0], goff[n)) is cut into gridDim.x equal 16-byte-aligned
 //     byte spans, one per 1024-thread workgroup (16 waves); a span may cross
 //     genome boundaries;
@@ -19,19 +19,18 @@
 //     (kf_index_records) and are invalid bytes (a k-mer reset).
 //
 // Kernels:
-//   K1  k1_kernel<K>   (k <= 6): 16-byte lanes, 1 KiB per wave iteration, one
-//       ds_add_u32 per window into a 4^k u32 histogram, two workgroups per CU;
-//   K1x k1x_kernel<7>  (k = 7): 3 KiB per wave iteration read as three
+//   K1x k1x_kernel<K>  (k = 2 .. 7): 3 KiB per wave iteration read as three
 //       coalesced 1 KiB regions (lane L: bytes 16L + 1024q, non-temporal
 //       buffer loads, xc_load); windows are formed per 16-byte region, the
-//       k-1 bases of context from lane L-1 by DPP.  Two consecutive 7-mer
-//       windows are one 8-mer counted once in P (65,536 u16 counters,
-//       128 KiB), a window left unpaired goes to S (16,384 u16 by forward
-//       7-mer, 32 KiB): half the LDS atomics of K1; every add returns the old
-//       word and a u16 half that reaches 0x4000 is moved to the count row
-//       (exact: see xc_fast);
+//       k-1 bases of context from lane L-1 by DPP.  Two consecutive k-mer
+//       windows are one (k+1)-mer counted once in P (4^(k+1) u16 counters:
+//       128 KiB at k = 7), a window left unpaired goes to S (4^k u16 by
+//       forward k-mer): half the LDS atomics of one add per window; every add
+//       returns the old word and a u16 half that reaches its threshold is moved
+//       to the count row (exact: see xc_fast);
 //   K1x8 k1x_kernel<8> (k = 8): the K1x front end with every window an 8-mer
 //       in P (one pass over the bytes).
+// (Rounds 1-3 counted k <= 6 with one u32 LDS add per window, K1.)
 // Rejected alternatives and their measurements live in tools/zoo/ (DESIGN.md).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -44,15 +43,13 @@
 
 namespace kf {
 
-constexpr int kBlock = 1024;             // threads per workgroup, both kernels
-constexpr int kWaves = kBlock / kWave;   // 16
+constexpr int kBlock = 1024;             // threads per workgroup
 // K1x: a genome piece's share per wave by the wave's age slot on its SIMD (the
 // SIMD issues oldest-first; slot 0 runs ~2.4x faster than slot 3), 8 bits each
 #ifndef KF_WAVE_WEIGHTS
 #define KF_WAVE_WEIGHTS (20u | 17u << 8 | 11u << 16 | 6u << 24)
 #endif
 constexpr uint32_t kWaveWeights = KF_WAVE_WEIGHTS;
-constexpr int kK1Ring = 4;   // K1: 1 KiB chunks in the register ring
 constexpr int kXRing = 2;    // K1x: 3 KiB iterations in the register ring
 
 __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
@@ -65,106 +62,6 @@ __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
 // memory another wave of the workgroup wrote).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// ---------------------------------------------------------------- K1 (k <= 6)
-// One 1 KiB chunk of a wave range: lane L owns bytes [16L, 16L+16).
-template <int K, bool MASKED>
-__device__ __forceinline__ uint32_t k1_chunk(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
-                                             const ChunkMask& m, uint64_t iv0, uint32_t carry, uint32_t& lane_total) {
-    constexpr uint32_t TM = (K > 1) ? ((1u << (2 * (K - 1))) - 1u) : 0u;
-    constexpr int W2 = 2 * K;
-    constexpr uint32_t M4 = ((1u << W2) - 1u) << 2;   // byte address of a forward code
-    if constexpr (!MASKED) {
-        // Fast case (uniform, the common one): every lane's 16 bytes are bases
-        // except at most one newline, and the carry is complete.  Then windows
-        // 0..ne-1 are valid and the context is lane L-1's raw codes: no validity
-        // masks, no tails, no run mask.
-        uint32_t Cf, NNL, bad;
-        classify16_fast(d, Cf, NNL, bad);
-        const uint32_t nef = (uint32_t)__builtin_popcount(NNL);
-        const bool self_ok = bad == 0 && nef >= 15u;
-        if (t_n(carry) >= (uint32_t)(K - 1) && __builtin_amdgcn_ballot_w64(!self_ok) == 0) {
-            // drop the newline entry (none: r = 16, identity)
-            const uint32_t r = (uint32_t)__builtin_ctz((NNL ^ 0xFFFFu) | 0x10000u);
-            const uint32_t lo1 = (1u << r) - 1u, lo2 = lo1 | (lo1 << r);
-            const uint32_t C = bfi(lo2, Cf, Cf >> 2);
-            const uint32_t pC = wave_shr1(t_codes(carry), C);
-            // X = (pC:C) << 2 over ne entries of C (ne in {15, 16}; C is zero
-            // above entry ne-1), so X's high word is pC << (2ne+2 mod 32) | C >> 30.
-            // Byte address of window r = bits [2r, 2r+2K+2) of X, masked: 8
-            // views at bit offsets 0,2,..,14 serve r = 0..7 from their low 16
-            // bits and r = 8..15 from their high 16 bits (a word select).
-            const uint32_t xlo = C << 2, xhi = (pC << ((2u * nef + 2u) & 31u)) | (C >> 30);
-            uint32_t xv[8];
-#pragma unroll
-            for (int o = 0; o < 8; ++o) xv[o] = o ? __builtin_amdgcn_alignbit(xhi, xlo, 2 * o) : xlo;
-            auto addr = [&](int w) -> uint32_t { return (w < 8 ? xv[w] : (xv[w - 8] >> 16)) & M4; };
-            const uint32_t inc15 = nef >> 4;   // window 15 exists iff no newline
-#pragma unroll
-            for (int w = 0; w < 15; ++w) lds_add(addr(w), 1u);
-            lds_add(addr(15), inc15);
-            lane_total += 15u + inc15;
-            // lane 63's block is all valid bases: its tail is complete
-            const uint32_t c63 = (uint32_t)__builtin_amdgcn_readlane((int)C, kWave - 1);
-            return tail_pack(c63 & TM, 31u, 31u);
-        }
-    }
-    uint32_t C, V, EN, ne, own;
-    front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
-    const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
-    const uint32_t xlo = win.wlo << 2, xhi = __builtin_amdgcn_alignbit(win.whi, win.wlo, 30);
-    uint32_t xv[8];
-#pragma unroll
-    for (int o = 0; o < 8; ++o) xv[o] = o ? __builtin_amdgcn_alignbit(xhi, xlo, 2 * o) : xlo;
-    auto addr = [&](int r) -> uint32_t { return (r < 8 ? xv[r] : (xv[r - 8] >> 16)) & M4; };
-#pragma unroll
-    for (int r = 0; r < 16; ++r) lds_add(addr(r), (win.R >> r) & 1u);
-    lane_total += (uint32_t)__builtin_popcount(win.R);
-    return win.next;
-}
-
-// The wave range [lo, hi) of genome [glo, ghi) in 1 KiB chunks (K1).
-template <int K>
-__device__ __forceinline__ uint32_t k1_range(const CountArgs& A, uint64_t glo, uint64_t ghi, uint64_t lo,
-                                             uint64_t hi, int lane) {
-    if (lo >= hi) return 0;
-    Range rg;
-    rg.init(glo, ghi, lo, hi);
-    // kK1Ring-deep register ring: a buffer is refilled only after it has been
-    // consumed, so no register rotation waits on a load; the first loads go out
-    // before the warm-up's dependent searches
-    uint4 buf[kK1Ring];
-#pragma unroll
-    for (int j = 0; j < kK1Ring; ++j) buf[j] = rg.load(A.bytes, j * kChunk, lane);
-    rg.warm<K>(A, lane);
-    uint32_t carry = rg.carry;
-    uint32_t rel = 0;
-    const ChunkMask m = rg.mask();
-    uint32_t lane_total = 0;
-    auto count = [&](const uint4 bf) {
-        const uint64_t cc = rg.c0 + rel;
-        if (rg.masked(A, rel))
-            carry = k1_chunk<K, true>(bf, A, cc, lane, m, rg.iv, carry, lane_total);
-        else
-            carry = k1_chunk<K, false>(bf, A, cc, lane, m, rg.iv, carry, lane_total);
-        rel += kChunk;
-    };
-    // steady state: groups of kK1Ring chunks with no exit in between (keeps the
-    // compiler's vmcnt bookkeeping exact: wait for the oldest load only)
-    const uint32_t nch = rg.nch;
-    for (uint32_t i = 0; i + kK1Ring <= nch; i += kK1Ring) {
-#pragma unroll
-        for (int j = 0; j < kK1Ring; ++j) {
-            count(buf[j]);
-            buf[j] = rg.load(A.bytes, rel + (kK1Ring - 1) * kChunk, lane);
-        }
-    }
-    const uint32_t rem = nch % kK1Ring;
-#pragma unroll
-    for (int j = 0; j < kK1Ring - 1; ++j)
-        if (rem > (uint32_t)j) count(buf[j]);
-    return lane_total;
-}
-
 // Byte span [lo, hi) of workgroup b of G over the batch (16-byte aligned).
 __device__ __forceinline__ void wg_span(const CountArgs& A, uint64_t& lo, uint64_t& hi) {
     const uint64_t base = A.goff[0];
@@ -174,72 +71,29 @@ __device__ __forceinline__ void wg_span(const CountArgs& A, uint64_t& lo, uint64
     hi = (b + 1 == G) ? base + total : base + ((total / G * (b + 1) + (total % G) * (b + 1) / G) & ~(uint64_t)15);
 }
 
+// ---------------------------------------------------------------- K1x (k = 2 .. 8)
+// LDS layout: P = u16 counters of (k+1)-mers at 0 ((k+1)-mer y in half y & 1 of
+// word y >> 1), then S = u16 singles by forward k-mer.  k = 7 takes the whole
+// 160 KiB of a CU (P 128 KiB, S 32 KiB); k = 8 counts every window as an 8-mer in
+// P (65,536 u16) and its S area only holds the flush's drain flags.
 template <int K>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) k1_kernel(CountArgs A) {
-    static_assert(K >= 2 && K <= 6, "K1 serves k <= 6");
-    constexpr uint32_t NCODES = 1u << (2 * K);
-    // dynamic LDS: the histogram at offset 0 (bin addresses need no base add),
-    // then one u64 reduction slot per wave; no static __shared__ (it would precede it)
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (uint32_t i = tid; i < NCODES; i += kBlock) hist[i] = 0;
-    __syncthreads();
-    unsigned long long* red = (unsigned long long*)(hist + NCODES);
-    if ((uint32_t)(uintptr_t)(lds_u32*)hist != 0u) __builtin_trap();   // lds_add assumes base 0
-    uint64_t span_lo, span_hi;
-    wg_span(A, span_lo, span_hi);
-    if (span_lo >= span_hi) return;
-    // first genome whose end is beyond span_lo
-    int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, span_lo, lane,
-                                          [&](uint64_t i) { return A.goff[i + 1]; });
-    for (; g < A.n_genomes; ++g) {
-        const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
-        if (glo >= span_hi) break;
-        const uint64_t plo = max(glo, span_lo), phi = min(ghi, span_hi);
-        if (phi <= plo) continue;
-        // wave w owns [split(w), split(w+1)): 16-byte aligned, monotone, covering [plo, phi)
-        const uint64_t lo = split_at(plo, phi, wave, kWaves), hi = split_at(plo, phi, wave + 1, kWaves);
-        (void)k1_range<K>(A, glo, ghi, lo, hi, lane);
-        __syncthreads();
-        // canonical bin = forward count of the k-mer + forward count of its
-        // revcomp; coalesced u32 atomics in column order, histogram re-zeroed
-        uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
-        unsigned long long s = 0;
-        for (uint32_t col = tid; col < A.nbins; col += kBlock) {
-            const uint32_t rep = A.col2rep[col];
-            const uint32_t rc = kf_revcomp<K>(rep);
-            const uint32_t v = hist[rep] + (rc != rep ? hist[rc] : 0u);
-            if (v) {
-                hist[rep] = 0;
-                hist[rc] = 0;
-                __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s += v;
-            }
-        }
-        s = wave_sum(s);
-        if (lane == 0) red[wave] = s;
-        __syncthreads();
-        if (tid == 0) {
-            unsigned long long t = 0;
-            for (int w = 0; w < kWaves; ++w) t += red[w];
-            if (t) atomicAdd(A.totals + g, t);
-        }
-    }
-}
-
-// ---------------------------------------------------------------- K1x (k = 7, 8)
-// LDS layout (the whole 160 KiB of a CU): P = 65,536 u16 counters at 0 (8-mer y
-// in half y & 1 of word y >> 1), then (k = 7) S = 16,384 u16 singles by forward
-// 7-mer; at k = 8 the S area only holds the flush's drain flags.
-constexpr uint32_t kPBytes = 1u << 17;                 // byte offset of S
-constexpr uint32_t kXLdsBytes = kPBytes + (1u << 15);  // 160 KiB
+struct XL {
+    static constexpr uint32_t P = K == 8 ? (1u << 17) : (2u << (2 * (K + 1)));   // P bytes = byte offset of S
+    static constexpr uint32_t S = K == 8 ? (1u << 15) : (2u << (2 * K));         // S bytes
+    static constexpr uint32_t bytes = P + S;                                      // dynamic LDS of the kernel
+};
 constexpr int kXChunk = 3 * kChunk;                    // bytes per wave iteration
 // u16 exactness (xc_fast): k = 7 checks every add's return against 0x4000 and
-// moves 0x4000 at a time; k = 8 (48 adds per lane per iteration) against 0x2000.
+// moves 0x4000 at a time; k = 8 (48 adds per lane per iteration) against 0x2000;
+// k <= 6 (small tables, frequent crossings) against 0x8000: a half then stays
+// below 0x8000 + 16 waves x 1536 adds = 0xE000.
 constexpr uint32_t kHot7 = 0xC000C000u, kStep7 = 0x4000u;
 constexpr uint32_t kHot8 = 0xE000E000u, kStep8 = 0x2000u;
+constexpr uint32_t kHot6 = 0x80008000u, kStep6 = 0x8000u;
+template <int K>
+constexpr uint32_t x_hot() { return K == 8 ? kHot8 : (K == 7 ? kHot7 : kHot6); }
+template <int K>
+constexpr uint32_t x_step() { return K == 8 ? kStep8 : (K == 7 ? kStep7 : kStep6); }
 
 __device__ __forceinline__ uint32_t half_one(uint32_t i) { return 1u << ((i & 1u) << 4); }
 
@@ -265,11 +119,12 @@ __device__ __forceinline__ uint32_t shl1_byte(uint32_t h, uint32_t one) {
 // Rare path: move STEP out of each half of the LDS word at byte address a that
 // has reached it (HOT = the halves' bits at or above STEP) into the count row,
 // until both halves are below STEP (compare-and-swap: exact under concurrent
-// adds).  k = 7: a P half is the 8-mer of two windows (older 7-mer = bin >> 2,
-// newer = bin & 0x3FFF), an S half one forward 7-mer; k = 8: a P half is one 8-mer.
+// adds).  k <= 7: a P half is the (k+1)-mer of two windows (older k-mer = bin >> 2,
+// newer = bin mod 4^k), an S half one forward k-mer; k = 8: a P half is one 8-mer.
 template <int K>
 __device__ __noinline__ void x_drain(uint32_t a, const uint32_t* __restrict__ code2col, uint32_t* gcounts) {
-    constexpr uint32_t HOT = K == 8 ? kHot8 : kHot7, STEP = K == 8 ? kStep8 : kStep7;
+    constexpr uint32_t HOT = x_hot<K>(), STEP = x_step<K>();
+    constexpr uint32_t PB = XL<K>::P;
     lds_u32* p = (lds_u32*)(uintptr_t)a;
     uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     while (cur & HOT) {
@@ -277,16 +132,16 @@ __device__ __noinline__ void x_drain(uint32_t a, const uint32_t* __restrict__ co
         uint32_t seen = cur;
         if (__hip_atomic_compare_exchange_strong(p, &seen, cur - sub, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            const bool single = a >= kPBytes;
-            const uint32_t w = (single ? a - kPBytes : a) >> 2;
+            const bool single = a >= PB;
+            const uint32_t w = (single ? a - PB : a) >> 2;
             for (uint32_t h = 0; h < 2; ++h) {
                 if (!((sub >> (16 * h)) & 0xFFFFu)) continue;
                 const uint32_t bin = 2 * w + h;
                 if (K == 8 || single) {
                     atomicAdd(gcounts + code2col[bin], STEP);
                 } else {
-                    atomicAdd(gcounts + code2col[bin >> 2], STEP);       // older 7-mer
-                    atomicAdd(gcounts + code2col[bin & 0x3FFFu], STEP);  // newer 7-mer
+                    atomicAdd(gcounts + code2col[bin >> 2], STEP);                      // older k-mer
+                    atomicAdd(gcounts + code2col[bin & ((1u << (2 * K)) - 1u)], STEP);  // newer k-mer
                 }
             }
             cur -= sub;
@@ -298,8 +153,8 @@ __device__ __noinline__ void x_drain(uint32_t a, const uint32_t* __restrict__ co
 // Drain every hot word of P (and S) -- one wave, the whole table.
 template <int K>
 __device__ __noinline__ void x_scan_drain(const uint32_t* __restrict__ code2col, uint32_t* gcounts, int lane) {
-    constexpr uint32_t HOT = K == 8 ? kHot8 : kHot7;
-    for (uint32_t w = (uint32_t)lane; w < (K == 8 ? kPBytes : kXLdsBytes) / 4; w += kWave) {
+    constexpr uint32_t HOT = x_hot<K>();
+    for (uint32_t w = (uint32_t)lane; w < (K == 8 ? XL<K>::P : XL<K>::bytes) / 4; w += kWave) {
         const uint32_t v = __hip_atomic_load((lds_u32*)(uintptr_t)(4 * w), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
         if (v & HOT) x_drain<K>(4 * w, code2col, gcounts);
@@ -421,10 +276,14 @@ __device__ __forceinline__ uint32_t wave_ror1(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);
 }
 
-// k = 7 adds of one region: pair j = windows 2j (newer) and 2j+1, the 8-mer at bits
-// [4j, 4j+16) of W; with a newline window 14 is left alone and goes to S.
-__device__ __forceinline__ void xc_pairs7(const XcWin& x, uint32_t (&rt)[8]) {
-    constexpr uint32_t PM = 0x1FFFCu;
+// k <= 7 adds of one region: pair j = windows 2j (newer) and 2j+1, the (k+1)-mer at
+// bits [4j, 4j+2k+2) of W; with a newline window 14 is left alone and goes to S.
+// Word addresses: P (k+1)-mer code x at (x >> 1) << 2 = (x << 1) & ~3, i.e. the
+// bits [4j, 4j+2k+3) of X = W << 1 masked by PM; an S k-mer likewise with SM.
+template <int K>
+__device__ __forceinline__ void xc_pairs(const XcWin& x, uint32_t (&rt)[8]) {
+    static_assert(K >= 2 && K <= 7, "pairs of k-mers: k <= 7");
+    constexpr uint32_t PM = (1u << (2 * K + 3)) - 4u, SM = (1u << (2 * K + 1)) - 4u;
     const uint32_t one = 1u;
     const uint32_t x0 = x.x0, y0 = x.y0;
     const uint32_t H0 = (x.c << 4) & 0x10101010u, H1 = x.c & 0x10101010u;
@@ -442,7 +301,7 @@ __device__ __forceinline__ void xc_pairs7(const XcWin& x, uint32_t (&rt)[8]) {
         rt[j] = lds_add_rtn(a, dl);
     }
     const uint32_t v = y0 >> 12;
-    const uint32_t a7 = bfi(0u - x.nl, kPBytes | (v & 0x7FFCu), v & PM);
+    const uint32_t a7 = bfi(0u - x.nl, XL<K>::P | (v & SM), v & PM);
     rt[7] = lds_add_rtn(a7, shl1_byte<3>(H1, one));
 }
 
@@ -479,7 +338,7 @@ __device__ __forceinline__ void xc_wins8(const XcWin& x, uint32_t (&rt)[16]) {
 template <int K>
 __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
                                         uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
-    constexpr uint32_t HOT = K == 8 ? kHot8 : kHot7;
+    constexpr uint32_t HOT = x_hot<K>();
     constexpr uint32_t TM = (1u << (2 * (K - 1))) - 1u;
     const XcCls k0 = xc_cls(d.q[0]), k1 = xc_cls(d.q[1]), k2 = xc_cls(d.q[2]);
     carry = __builtin_amdgcn_readfirstlane(carry);
@@ -489,12 +348,12 @@ __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int
     const XcWin x0 = xc_window(k0, t_codes(carry));
     const XcWin x1 = xc_window(k1, wave_ror1(x0.c));
     const XcWin x2 = xc_window(k2, wave_ror1(x1.c));
-    if constexpr (K == 7) {
+    if constexpr (K <= 7) {
         const XcWin* xs[3] = {&x0, &x1, &x2};
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             uint32_t r[8];
-            xc_pairs7(*xs[i], r);
+            xc_pairs<K>(*xs[i], r);
 #pragma unroll
             for (int j = 0; j < 8; j += 4) o |= r[j] | r[j + 1] | r[j + 2] | r[j + 3];
         }
@@ -524,7 +383,7 @@ template <int K, bool MASKED>
 __device__ __forceinline__ uint32_t x_singles(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
                                               const ChunkMask& m, uint64_t iv0, uint32_t carry, uint32_t* gcounts,
                                               uint32_t& lane_total, uint32_t& drained) {
-    constexpr uint32_t HOT = K == 8 ? kHot8 : kHot7;
+    constexpr uint32_t HOT = x_hot<K>();
     uint32_t C, V, EN, ne, own;
     front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
     const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
@@ -536,7 +395,7 @@ __device__ __forceinline__ uint32_t x_singles(const uint4 d, const CountArgs& A,
     for (int r = 0; r < 16; ++r) {
         const int fo = (2 * r) & ~7;
         const uint32_t y = __builtin_amdgcn_ubfe(wv[fo >> 3], 2 * r - fo, 2 * K);
-        o |= lds_add_rtn((K == 8 ? 0u : kPBytes) + ((y >> 1) << 2), ((R >> r) & 1u) * half_one(y));
+        o |= lds_add_rtn((K == 8 ? 0u : XL<K>::P) + ((y >> 1) << 2), ((R >> r) & 1u) * half_one(y));
     }
     if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
         x_scan_drain<K>(A.code2col, gcounts, lane);
@@ -640,9 +499,30 @@ __device__ __forceinline__ void pair_f_sums(const uint32_t* hist, int tid, uint3
     }
 }
 
+// k <= 6 flush (1024 threads): F(y) for the 4^k forward k-mers, thread t owning
+// y = t + 1024 m: sum_a P[4y + a] (two words) + sum_a P[a 4^k + y] + S[y].
+template <int K>
+__device__ __forceinline__ void pair_f_sums_small(const uint32_t* hist, int tid,
+                                                  uint32_t (&F)[((1u << (2 * K)) + kBlock - 1) / kBlock]) {
+    constexpr uint32_t NY = 1u << (2 * K), NM = (NY + kBlock - 1) / kBlock;
+#pragma unroll
+    for (uint32_t m = 0; m < NM; ++m) {
+        const uint32_t y = (uint32_t)tid + kBlock * m;
+        F[m] = 0;
+        if (y < NY) {
+            const uint32_t sh = (y & 1u) << 4;
+            uint32_t f = u16sum2(hist[2 * y]) + u16sum2(hist[2 * y + 1]);   // y older: P[4y .. 4y + 3]
+#pragma unroll
+            for (uint32_t a = 0; a < 4; ++a) f += (hist[a * (NY / 2) + (y >> 1)] >> sh) & 0xFFFFu;   // y newer
+            f += (hist[XL<K>::P / 4 + (y >> 1)] >> sh) & 0xFFFFu;                                    // single
+            F[m] = f;
+        }
+    }
+}
+
 template <int K>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) k1x_kernel(CountArgs A) {
-    static_assert(K == 7 || K == 8, "K1x serves k = 7 and 8");
+    static_assert(K >= 2 && K <= 8, "K1x serves k = 2 .. 8");
     // P and S (the whole dynamic LDS, at address 0: see lds_add); no LDS is left
     // for reduction slots, so totals go straight to global atomics
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
@@ -651,7 +531,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     {
         uint4* h4 = (uint4*)hist;
-        for (uint32_t i = tid; i < kXLdsBytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (uint32_t i = tid; i < XL<K>::bytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
     }
     __syncthreads();
     if ((uint32_t)(uintptr_t)(lds_u32*)hist != 0u) __builtin_trap();   // lds_add assumes base 0
@@ -681,9 +561,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 
             // canonical 8-mer column = P[rep] + P[rc rep] (a palindrome once);
             // drain flags in the (unused) S area
             lds_barrier();   // every add of this piece is done
-            if (lane == 0) hist[kPBytes / 4 + wave] = drained;
+            if (lane == 0) hist[XL<K>::P / 4 + wave] = drained;
             lds_barrier();
-            const uint4* fl = (const uint4*)(hist + kPBytes / 4);
+            const uint4* fl = (const uint4*)(hist + XL<K>::P / 4);
             const uint4 f0 = fl[0], f1 = fl[1], f2 = fl[2], f3 = fl[3];
             const bool any_drain = (f0.x | f0.y | f0.z | f0.w | f1.x | f1.y | f1.z | f1.w | f2.x | f2.y | f2.z |
                                     f2.w | f3.x | f3.y | f3.z | f3.w) != 0;
@@ -698,7 +578,52 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 
             }
             lds_barrier();   // columns read
             uint4* h4 = (uint4*)hist;
-            for (uint32_t i = tid; i < kXLdsBytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+            for (uint32_t i = tid; i < XL<K>::bytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+        } else if constexpr (K <= 6) {
+            // canonical column = F(rep) + F(rc rep) (a palindrome once, even k);
+            // F = pair and single sums (pair_f_sums_small), back in LDS words
+            // [0, 4^k) (swizzled as f_swz), the drain flags after them
+            constexpr uint32_t NY = 1u << (2 * K), NM = (NY + kBlock - 1) / kBlock;
+            constexpr uint32_t NCOL = (NY + (K % 2 == 0 ? (1u << K) : 0u)) / 2, NC = (NCOL + kBlock - 1) / kBlock;
+            uint32_t rep[NC];
+#pragma unroll
+            for (uint32_t c = 0; c < NC; ++c) {
+                const uint32_t col = (uint32_t)tid + c * kBlock;
+                rep[c] = col < NCOL ? A.col2rep[col] : 0u;
+            }
+            lds_barrier();   // every add of this piece is done
+            uint32_t F[NM];
+            pair_f_sums_small<K>(hist, tid, F);
+            lds_barrier();   // P and S read
+#pragma unroll
+            for (uint32_t m = 0; m < NM; ++m) {
+                const uint32_t y = (uint32_t)tid + kBlock * m;
+                if (y < NY) hist[f_swz(y)] = F[m];
+            }
+            if (lane == 0) hist[NY + wave] = drained;   // (P holds 2 x 4^k words: past F is free)
+            lds_barrier();   // F in LDS words [0, 4^k), drain flags after it
+            const uint4* fl = (const uint4*)(hist + NY);
+            const uint4 f0 = fl[0], f1 = fl[1], f2 = fl[2], f3 = fl[3];
+            const bool any_drain = (f0.x | f0.y | f0.z | f0.w | f1.x | f1.y | f1.z | f1.w | f2.x | f2.y | f2.z | f2.w |
+                                    f3.x | f3.y | f3.z | f3.w) != 0;
+            uint32_t cv[NC];
+#pragma unroll
+            for (uint32_t c = 0; c < NC; ++c) {
+                const uint32_t y = rep[c], rc = kf_revcomp<K>(y);
+                cv[c] = hist[f_swz(y)] + (rc != y ? hist[f_swz(rc)] : 0u);
+            }
+            lds_barrier();   // columns read
+            uint4* h4 = (uint4*)hist;
+            for (uint32_t i = tid; i < XL<K>::bytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (uint32_t c = 0; c < NC; ++c) {
+                const uint32_t col = (uint32_t)tid + c * kBlock;
+                if (col >= NCOL) continue;
+                if (whole && !any_drain)
+                    __builtin_nontemporal_store(cv[c], gc + col);
+                else if (cv[c])
+                    __hip_atomic_fetch_add(gc + col, cv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         } else {
             // the columns' forward representatives, loaded before the barrier so
             // their latency overlaps it.  A whole genome takes four consecutive
@@ -718,7 +643,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 
             pair_f_sums(hist, tid, F);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {   // singles of y = 2048 i + 2 tid + {0, 1}
-                const uint32_t v = hist[kPBytes / 4 + i * 1024 + tid];
+                const uint32_t v = hist[XL<K>::P / 4 + i * 1024 + tid];
                 F[2 * i] += v & 0xFFFFu;
                 F[2 * i + 1] += v >> 16;
             }
@@ -739,7 +664,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 
             }
             lds_barrier();   // columns read
             uint4* h4 = (uint4*)hist;
-            for (uint32_t i = tid; i < kXLdsBytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+            for (uint32_t i = tid; i < XL<K>::bytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
             // the row writes last: their issue overlaps the zeroing, the barrier
             // and the next piece's setup
             if (whole && !any_drain) {
@@ -889,11 +814,11 @@ namespace {
 
 void* kernel_for(int k) {
     switch (k) {
-    case 2: return (void*)&k1_kernel<2>;
-    case 3: return (void*)&k1_kernel<3>;
-    case 4: return (void*)&k1_kernel<4>;
-    case 5: return (void*)&k1_kernel<5>;
-    case 6: return (void*)&k1_kernel<6>;
+    case 2: return (void*)&k1x_kernel<2>;
+    case 3: return (void*)&k1x_kernel<3>;
+    case 4: return (void*)&k1x_kernel<4>;
+    case 5: return (void*)&k1x_kernel<5>;
+    case 6: return (void*)&k1x_kernel<6>;
     case 7: return (void*)&k1x_kernel<7>;
     case 8: return (void*)&k1x_kernel<8>;
     default: return nullptr;
@@ -901,7 +826,17 @@ void* kernel_for(int k) {
 }
 
 // K1: histogram (4^k u32) + one u64 reduction slot per wave; K1x: P + S
-int lds_bytes_for(int k) { return k <= 6 ? (int)(sizeof(uint32_t) << (2 * k)) + 8 * kWaves : (int)kXLdsBytes; }
+int lds_bytes_for(int k) {
+    switch (k) {
+    case 2: return (int)XL<2>::bytes;
+    case 3: return (int)XL<3>::bytes;
+    case 4: return (int)XL<4>::bytes;
+    case 5: return (int)XL<5>::bytes;
+    case 6: return (int)XL<6>::bytes;
+    case 7: return (int)XL<7>::bytes;
+    default: return (int)XL<8>::bytes;
+    }
+}
 
 // grid per (k, device): workgroups per CU from the occupancy API x CUs
 int g_grid[KF_MAX_K + 1][64];

@@ -534,15 +534,27 @@ def get_chunks(args) -> None:
 
     def report(genomes):
         for gm in genomes:
-            log.info("\n==> Start processing. Sample: {}".format(gm.fname))
-            if gm.excluded == "none":                                    # main.py:761-778
+            log.info("\n==> Start processing. Sample: {}".format(gm.fname))                   # main.py:703
+            log.info(">>> Formatting to single line. Sample: {}".format(gm.fname))            # :728
+            log.info(">>> Replacing stretches of N. Sample: {}".format(gm.fname))             # :737
+            log.info(">>> Filtering contigs below threshold {}. Sample: {}".format(CH.CHUNK_SZ, gm.fname))   # :746
+            if gm.excluded == "none":                                                         # :761-778
                 stamp("\n==> Excluded {}. No contigs above threshold length.".format(gm.fname))
-            elif gm.excluded == "few":                                   # main.py:845-860
+                continue
+            log.info(">>> Splitting into contigs. Sample: {}".format(gm.fname))               # :783
+            log.info(">>> Getting contig ids. Sample: {}".format(gm.fname))                   # :789
+            log.info(">>> Computing contig statistics. Sample: {}".format(gm.fname))          # :799
+            if gm.excluded == "few":                                                          # :845-860
                 stamp("\n==> Excluded {}. {} chunks is too low. {} is required.".format(
                     gm.fname, len(gm.names), CH.CHUNK_CNT_THR))
-            else:
-                stamp("\n==> Done chunk processing for {}.".format(gm.fname))
-                stamp("\n==> Done computing k-mer frequences for {}.".format(gm.fname))
+                continue
+            stamp("\n==> Done chunk processing for {}.".format(gm.fname))                    # :866
+            # the reference runs get_frequencies on the genome's chunk directory here
+            # (main.py:869-881), which prints its first and last lines to stdout
+            chunk_dir = os.path.join(args.output_dir, "{}_chunks".format(gm.sample))
+            print("\n==> Starting k-mer counting for {}\n".format(chunk_dir))
+            print("\n==> Done processing {}".format(chunk_dir))
+            stamp("\n==> Done computing k-mer frequences for {}.".format(gm.fname))          # :885
 
     nxt = reader.submit(read, batches[0]) if batches else None
     prev = None   # (genomes, write futures) of the previous batch, logged once written
