@@ -74,14 +74,13 @@ namespace kf {
 #ifndef KF_BK_PRE2_MAXK   // KF_BK_PRE2 applies to k <= this
 #define KF_BK_PRE2_MAXK 10
 #endif
-// u16 phase-2 histograms: when no bucket of a piece has 65,536 records (phase 1
-// sums the round counts), each bin is a u16 half, even buckets in the low and odd
-// buckets in the high halves of the 32,768 words.  A bucket's flush (ds_and_rtn
-// clearing its half) then overlaps the next bucket's adds into the other half,
-// with one barrier per bucket instead of two.  Otherwise (skewed pieces, and
-// k <= 10 whose few buckets hold more records) the u32 path.
-#ifndef KF_BK_U16
-#define KF_BK_U16 1
+// Phase-2 rounds per wave: 0 = dealt round-robin (round wave + W j); otherwise a
+// contiguous block of rounds per wave, its size proportional to byte (wave >> 2)
+// of KF_BK_RW (the wave's age slot on its SIMD, as K1x's KF_WAVE_WEIGHTS): the
+// SIMD issues its oldest wave first, so equal shares leave the older waves
+// waiting at every bucket barrier for the youngest.
+#ifndef KF_BK_RW
+#define KF_BK_RW 0
 #endif
 constexpr uint32_t kBkSlots = KF_BK_LAG ? 2u : 1u;   // record / meta / roff slots per workgroup
 // Wave priority by age slot (tools/ A/B builds): bit 0 = phase 1, bit 1 = phase 2
@@ -215,9 +214,6 @@ __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
 }
 __device__ __forceinline__ uint32_t lds_xchg(uint32_t a, uint32_t v) {
     return __hip_atomic_exchange((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ uint32_t lds_and_rtn(uint32_t a, uint32_t v) {
-    return __hip_atomic_fetch_and((lds_u32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // Byte address (x 4) of the record in u16 half h of d: one SDWA shift.
 __device__ __forceinline__ uint32_t rec_addr(uint32_t d, int h) {
@@ -418,7 +414,6 @@ bucket_kernel(CountArgs A, BucketArgs B) {
         return P;
     };
 
-    uint32_t u16ok = 0;   // bit s: the piece in record slot s may count in u16 halves (wave-uniform)
     for (uint32_t it = 0; it < nmine + lag; ++it) {
       if (it < nmine) {
         const uint32_t slot = kLagK ? (it & 1u) : 0u;
@@ -477,9 +472,6 @@ bucket_kernel(CountArgs A, BucketArgs B) {
 #endif
             }
         };
-        uint32_t acc[L::epl];   // this lane's rank entries, summed over the piece's rounds
-#pragma unroll
-        for (uint32_t e = 0; e < L::epl; ++e) acc[e] = 0;
         auto round = [&](uint32_t r, uint4& bf) {
             const uint32_t cb = L::cnt + 4 * L::nent * (r % 3);
             const uint32_t cz = L::cnt + 4 * L::nent * ((r + 1) % 3);
@@ -545,8 +537,6 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             constexpr uint32_t BPL = NR >= EPL ? 1u : EPL / NR;   // buckets described by this lane
             uint32_t c[EPL];
             lds_ldn<EPL>(cb + 4 * EPL * lane, c);
-#pragma unroll
-            for (uint32_t e = 0; e < EPL; ++e) acc[e] += c[e];
             uint32_t o[EPL];               // offsets of the lane's entries
             uint32_t T;                    // padded records of the round
             uint32_t bst[BPL], bcnt[BPL];  // run start and record count of the lane's buckets
@@ -672,15 +662,6 @@ bucket_kernel(CountArgs A, BucketArgs B) {
         if (r < nround) round(r++, buf[2]);
         lds_barrier();
         if (nround > 0) copy_out(nround - 1, t_prev, off_prev);
-        {
-            // a bin holds at most its bucket's records: the bucket's replicas summed
-            // (bounded by nrep x the largest entry) below 65,536 -> u16 halves
-            uint32_t mx = 0;
-#pragma unroll
-            for (uint32_t e = 0; e < L::epl; ++e) mx = max(mx, acc[e]);
-            const bool big = __builtin_amdgcn_ballot_w64(mx * L::nrep > 65535u) != 0;
-            u16ok = (u16ok & ~(1u << slot)) | ((KF_BK_U16 && !big) ? (1u << slot) : 0u);
-        }
         if (B.prof && tid == 0) B.prof[8 * blockIdx.x] += __builtin_amdgcn_s_memtime() - t_p1;
         if (B.prof && lane == 0) B.prof[8 * gridDim.x + 4 * (W * blockIdx.x + wave) + 2] += p1w;
       }
@@ -703,9 +684,6 @@ bucket_kernel(CountArgs A, BucketArgs B) {
         lds_barrier();
         uint32_t* row = A.counts + (uint64_t)g * A.nbins;
         const bool split = np > 1;
-        const bool h16 = ((u16ok >> slot) & 1u) != 0;   // u16 halves for this piece
-        bool hodd = false;                               // current bucket in the high halves
-        uint32_t hkeep = 0;                              // and_rtn mask keeping the other half
         unsigned long long tsum = 0;
         // Run table of this wave: run j (< nrun) <-> round wave + W j, held by lane
         // j mod 64 in half j / 64 (W = 8 needs up to 128 runs).  A run is the whole
@@ -720,10 +698,21 @@ bucket_kernel(CountArgs A, BucketArgs B) {
         bool myr_ok[H];
         uint32_t myr_c[H], ro[H];
         uint32_t nrun = 0;
+        constexpr bool kRw = KF_BK_RW != 0 && W == 16;
+        uint32_t rw0 = 0, rw1 = 0;   // kRw: this wave's rounds [rw0, rw1)
+        if constexpr (kRw) {
+            constexpr uint32_t wts = (uint32_t)KF_BK_RW;
+            constexpr uint32_t w0 = wts & 0xFFu, w1 = (wts >> 8) & 0xFFu, w2 = (wts >> 16) & 0xFFu, w3 = wts >> 24;
+            constexpr uint32_t m01 = w0 > w1 ? w0 : w1, m23 = w2 > w3 ? w2 : w3, mx = m01 > m23 ? m01 : m23;
+            constexpr uint32_t tot = 4u * (w0 + w1 + w2 + w3);
+            static_assert((uint64_t)L::rmax * mx <= (uint64_t)tot * 64u * H - tot, "a wave's rounds must fit its run table");
+            rw0 = (nround * wave_frac((uint32_t)wave, wts)) >> 20;
+            rw1 = (nround * wave_frac((uint32_t)wave + 1, wts)) >> 20;
+        }
 #pragma unroll
         for (int h = 0; h < H; ++h) {
-            const uint32_t myr = (uint32_t)wave + (uint32_t)W * (64u * h + (uint32_t)lane);
-            myr_ok[h] = myr < nround;
+            const uint32_t myr = kRw ? rw0 + 64u * h + (uint32_t)lane : (uint32_t)wave + (uint32_t)W * (64u * h + (uint32_t)lane);
+            myr_ok[h] = kRw ? myr < rw1 : myr < nround;
             myr_c[h] = myr_ok[h] ? myr : 0u;
             nrun += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(myr_ok[h]));
             const uint32_t ro_l = __builtin_nontemporal_load(roff + myr_c[h]);
@@ -801,7 +790,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             }
             t.w0 += kGW * kWave;
         };
-        auto consume = [&](const Grp& G, uint32_t U, uint32_t pm, uint32_t inc) {   // pm: bucket parity mask
+        auto consume = [&](const Grp& G, uint32_t U, uint32_t pm) {   // pm: bucket parity mask
 #pragma unroll
             for (int x = 0; x < kGW; ++x) {
                 if (G.w0 + x * kWave >= U) break;   // wave-uniform
@@ -811,7 +800,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
                     asm volatile("" ::"v"(d[0]), "v"(d[1]), "v"(d[2]), "v"(d[3]));
 #else
 #pragma unroll
-                    for (int t = 0; t < 8; ++t) lds_add(rec_addr(d[t >> 1], t & 1), inc);
+                    for (int t = 0; t < 8; ++t) lds_add(rec_addr(d[t >> 1], t & 1), 1u);
 #endif
                 }
             }
@@ -850,15 +839,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const uint32_t col = g4 + t;
-                const uint32_t a = ((ci[t >> 1] >> (16 * (t & 1))) & 0xFFFFu) << 2;
-                if (!(col >= c0 && col < c1)) {
-                    v[t] = 0u;
-                } else if (h16) {   // read and clear this bucket's half only
-                    const uint32_t o = lds_and_rtn(a, hkeep);
-                    v[t] = hodd ? o >> 16 : o & 0xFFFFu;
-                } else {
-                    v[t] = lds_xchg(a, 0u);
-                }
+                v[t] = (col >= c0 && col < c1) ? lds_xchg(((ci[t >> 1] >> (16 * (t & 1))) & 0xFFFFu) << 2, 0u) : 0u;
                 tsum += v[t];
             }
             if (!split && !B.accumulate && g4 >= c0 && g4 + 4 <= c1) {
@@ -900,9 +881,6 @@ bucket_kernel(CountArgs A, BucketArgs B) {
         for (uint32_t b = 0; b < (KF_BK_ABL == 8 ? 0u : NBK); ++b) {   // (ABL 8: phase 1 only)
             uint64_t t0 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
             const uint32_t pm = ((b & L::hmask) << L::bits) * 0x10001u;   // both records of a word
-            hodd = (b & 1u) != 0;
-            hkeep = hodd ? 0x0000FFFFu : 0xFFFF0000u;
-            const uint32_t inc = h16 && hodd ? 0x10000u : 1u;   // this bucket's half
 #if KF_BK_DB
             // two groups alternate: the bucket's next group is always in flight
             // while one is counted (issued unconditionally -- past the bucket's
@@ -911,28 +889,28 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             if constexpr (kPre2) {
                 // both groups were issued before the previous flush
                 for (;;) {
-                    consume(G0, tb.U, pm, inc);
+                    consume(G0, tb.U, pm);
                     if (G1.w0 >= tb.U) break;
                     issue(tb, G0);
-                    consume(G1, tb.U, pm, inc);
+                    consume(G1, tb.U, pm);
                     if (G0.w0 >= tb.U) break;
                     issue(tb, G1);
                 }
             } else {
                 for (;;) {
                     issue(tb, G1);
-                    consume(G0, tb.U, pm, inc);
+                    consume(G0, tb.U, pm);
                     if (G1.w0 >= tb.U) break;
                     issue(tb, G0);
-                    consume(G1, tb.U, pm, inc);
+                    consume(G1, tb.U, pm);
                     if (G0.w0 >= tb.U) break;
                 }
             }
 #else
-            consume(G0, tb.U, pm, inc);
+            consume(G0, tb.U, pm);
             while (tb.w0 < tb.U) {   // a bucket beyond one group: synchronous groups
                 issue(tb, G0);
-                consume(G0, tb.U, pm, inc);
+                consume(G0, tb.U, pm);
             }
 #endif
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tcons += __builtin_amdgcn_s_memtime() - t0; }
@@ -959,10 +937,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             for (uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + kFG * L::block); g4 < c1; g4 += 4 * L::block)
                 flush_cols(g4, col_at(g4), c0, c1);
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[2] += t - t0; t0 = t; }
-            // u32 bins: the flush must finish before the next bucket's adds; u16
-            // halves: the next bucket counts into the other half, and the barrier
-            // after its adds orders this flush before bucket b + 2's
-            if (!h16) lds_barrier();
+            lds_barrier();
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[3] += t - t0; }
         }
         if (B.prof && lane == 0) {   // per wave: records, barrier, (phase-1 barrier), consume

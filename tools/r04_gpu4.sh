@@ -19,4 +19,5 @@ LIB=tools/ab/libkf2vec_new.so K=11 TAG=r04/v4_pmc_k11_full GROUPS_LIST="$G1"$'\n
 LIB=tools/ab/libkf2vec_abl8.so K=11 TAG=r04/v4_pmc_k11_phase1 GROUPS_LIST="$G1"$'\n'"$G2" bash tools/r04_pmc.sh &&
 python3 tools/pmc_summary.py gpurun_out/r04/v4_pmc_k11_full bucket_kernel > gpurun_out/r04/v4_pmc_k11_full.txt &&
 python3 tools/pmc_summary.py gpurun_out/r04/v4_pmc_k11_phase1 bucket_kernel > gpurun_out/r04/v4_pmc_k11_phase1.txt &&
-timeout -k 10 200 python -u tools/r04_e2e_trace.py --parts 2,4,8,16 > gpurun_out/r04/v4_e2e_trace.json 2> gpurun_out/r04/v4_e2e_trace.err
+timeout -k 10 200 python -u tools/r04_e2e_trace.py --parts 2,4,8,16 > gpurun_out/r04/v4_e2e_trace.json 2> gpurun_out/r04/v4_e2e_trace.err &&
+timeout -k 10 60 ./tools/bin/lds_ops > gpurun_out/r04/v4_lds_ops.txt 2>&1
