@@ -182,13 +182,17 @@ int kf_write_kf_rows(const char* path, const char* const* names, int32_t n,
                      int raw_cnt, int n_threads);
 
 /* get_chunks, many genomes at once: segment g is rows [seg_row0[g],
- * seg_row0[g+1]) of counts / names (seg_row0[0] = 0, non-decreasing), written
- * in row order to paths[g], appended if seg_append && seg_append[g] (a genome
- * whose windows span several count launches), else truncated.  Rows are
- * formatted by n_threads host threads, then the segment files are written by
- * up to n_threads threads (one file each at a time). */
+ * seg_row0[g+1]) of counts (seg_row0[0] = 0, non-decreasing), written in row
+ * order to paths[g] (distinct), appended if seg_append && seg_append[g] (a genome
+ * whose windows span several count launches), else truncated.  Row i is named
+ * names[i], or, with names == NULL, prefixes[row_prefix[i]] followed by
+ * "<s+1>-<s+win_len>" for s = row_start[i] (the window names of main.py:905-915).
+ * n_threads host threads format rows into private arenas and write each
+ * segment's file once its rows are formatted (formatting and writing overlap). */
 int kf_write_kf_segments(int32_t n_seg, const char* const* paths, const int32_t* seg_row0,
                          const uint8_t* seg_append, const char* const* names,
+                         const char* const* prefixes, const uint32_t* row_prefix,
+                         const uint64_t* row_start, uint32_t win_len,
                          const uint32_t* counts, uint64_t nbins, int pseudocount,
                          int raw_cnt, int n_threads);
 

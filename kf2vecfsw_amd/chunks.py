@@ -39,6 +39,17 @@ from . import _native as N
 
 CHUNK_SZ = 10000       # main.py:100
 CHUNK_CNT_THR = 5      # main.py:101
+LAUNCH_WINDOWS = 4096  # windows per count launch at most (128 MiB of k=7 counts)
+
+# KF_TRACE=1: stage timeline (host ms since the first event) for tools/chunks_bench.py
+TRACE = os.environ.get("KF_TRACE") == "1"
+trace: list = []
+
+
+def _tr(stage: str, t0: float, **kw) -> None:
+    if TRACE:
+        import time
+        trace.append((stage, round(t0 * 1e3, 3), round(time.perf_counter() * 1e3, 3), kw))
 
 
 def window_plan(total_length: int) -> tuple[int, int]:
@@ -105,15 +116,31 @@ def record_regions(data: np.ndarray) -> tuple[np.ndarray, list[str]]:
 
 @dataclass
 class Genome:
-    """One input file of a batch and its fate (the log lines of main.py:761-885)."""
+    """One input file of a batch and its fate (the log lines of main.py:761-885).
+    Window w starts at starts[w] in the batch's processed sequence and at wpos[w]
+    in its contig, whose name prefix is prefixes[wpre[w]]."""
     fname: str
     sample: str
     rec_lo: int = 0                  # its records in the batch's record table
     rec_hi: int = 0
-    names: list = field(default_factory=list)
-    starts: np.ndarray | None = None  # window starts in the batch's processed sequence
+    prefixes: list = field(default_factory=list)   # "<sample>.part_<cid>.part_<cid>_sliding__" per contig
+    wpre: np.ndarray | None = None
+    wpos: np.ndarray | None = None
+    starts: np.ndarray | None = None
     excluded: str | None = None       # "none" (no contig >= 10 kbp) or "few"
     write: bool = True                # False: a later file has the same sample name
+
+    @property
+    def n_windows(self) -> int:
+        return 0 if self.starts is None else int(self.starts.size)
+
+    @property
+    def names(self) -> list[str]:
+        """Row names (main.py:905-915), built here only for tests: the writer builds them."""
+        if self.starts is None:
+            return []
+        return [self.prefixes[int(p)] + "{}-{}".format(int(s) + 1, int(s) + CHUNK_SZ)
+                for p, s in zip(self.wpre, self.wpos)]
 
 
 class ChunkPipeline:
@@ -135,6 +162,8 @@ class ChunkPipeline:
         """Compact every record of the batch on the device and plan the windows of
         every genome (one device-to-host copy).  Fills genomes[i].names/starts/
         excluded; returns the processed sequence buffer (device)."""
+        import time
+        t0 = time.perf_counter()
         data = hb.data.numpy()
         rec_se: list[int] = []
         rec_ids: list[str] = []
@@ -150,6 +179,8 @@ class ChunkPipeline:
             rec_ids += ids
             gm.rec_hi = len(rec_ids)
         n_rec = len(rec_ids)
+        _tr("records", t0, n_rec=n_rec)
+        t0 = time.perf_counter()
         dev = self.device
         stream = torch.cuda.current_stream(dev)
         total = int(hb.off[-1])
@@ -169,8 +200,10 @@ class ChunkPipeline:
             out_se = d_se.cpu().numpy().view(np.uint64)      # the batch's one synchronising copy
         else:
             out_se = np.zeros(0, np.uint64)
+        _tr("h2d_compact_d2h", t0, bytes=total)
+        t0 = time.perf_counter()
         for gm in genomes:
-            names, starts = [], []
+            starts, pos_l, pre_l = [], [], []
             for r in range(gm.rec_lo, gm.rec_hi):
                 a, b = int(out_se[2 * r]), int(out_se[2 * r + 1])
                 L = b - a
@@ -180,14 +213,15 @@ class ChunkPipeline:
                 cid = rec_ids[r]
                 pos = np.arange(n, dtype=np.int64) * step
                 starts.append(a + pos)
-                pre = "{}.part_{}.part_{}_sliding__".format(gm.sample, cid, cid)
-                names += [pre + "{}-{}".format(p + 1, p + CHUNK_SZ) for p in pos.tolist()]
+                pos_l.append(pos)
+                pre_l.append(np.full(n, len(gm.prefixes), np.uint32))
+                gm.prefixes.append("{}.part_{}.part_{}_sliding__".format(gm.sample, cid, cid))
+            cat = (lambda x, t: np.concatenate(x) if x else np.zeros(0, t))
+            gm.starts, gm.wpos, gm.wpre = cat(starts, np.int64), cat(pos_l, np.int64), cat(pre_l, np.uint32)
             if not starts:
                 gm.excluded = "none"                               # main.py:761-778
-            elif len(names) < CHUNK_CNT_THR:
+            elif gm.n_windows < CHUNK_CNT_THR:
                 gm.excluded = "few"                                # main.py:845-860
-            gm.names = names
-            gm.starts = np.concatenate(starts) if starts else np.zeros(0, np.int64)
         # the reference writes genome by genome, so a later file with the same
         # sample name replaces an earlier one's .kf: inside a batch, only the last
         # written one is counted (across batches the in-order writer does it)
@@ -196,6 +230,7 @@ class ChunkPipeline:
             if gm.excluded is None:
                 gm.write = gm.sample not in kept
                 kept.add(gm.sample)
+        _tr("plan", t0, windows=sum(g.n_windows for g in genomes))
         return d_out
 
     # ------------------------------------------------------------ count + write
@@ -210,7 +245,7 @@ class ChunkPipeline:
         dev = self.device
         # flat window list of the batch, with its genome boundaries
         starts = np.concatenate([g.starts for g in work]).astype(np.int64)
-        row0 = np.cumsum([0] + [len(g.names) for g in work])
+        row0 = np.cumsum([0] + [g.n_windows for g in work])
         total = int(row0[-1])
         d_starts = torch.from_numpy(starts).pin_memory().to(dev, non_blocking=True)
         stream = torch.cuda.current_stream(dev)
@@ -235,8 +270,8 @@ class ChunkPipeline:
                 a, b = max(int(row0[gi]), w0), min(int(row0[gi + 1]), w1)
                 if a >= b:
                     continue
-                segs.append((os.path.join(output_dir, "{}.kf".format(g.sample)), a - w0, b - w0,
-                             g.names[a - int(row0[gi]): b - int(row0[gi])], a > int(row0[gi])))
+                segs.append((os.path.join(output_dir, "{}.kf".format(g.sample)), a - w0, b - w0, g,
+                             a - int(row0[gi]), a > int(row0[gi])))
             if len(self.pending) >= 2:      # at most two launches queued for the writer
                 self.pending.pop(0).result()
             futs.append(self.writer.submit(self._write, ev, host, segs))
@@ -246,18 +281,34 @@ class ChunkPipeline:
 
     def _write(self, ev, host: torch.Tensor, segs) -> None:
         """Format + write one launch's rows (segments are consecutive row ranges)."""
+        import time
+        t0 = time.perf_counter()
         ev.synchronize()
+        _tr("wait_d2h", t0)
+        t0 = time.perf_counter()
         if not segs:
             return
         rows = host.numpy().view(np.uint32)
         paths = (ctypes.c_char_p * len(segs))(*[os.fsencode(s[0]) for s in segs])
         row0 = np.asarray([0] + [s[2] for s in segs], dtype=np.int32)
-        app = np.asarray([1 if s[4] else 0 for s in segs], dtype=np.uint8)
-        enc = [n.encode(errors="surrogateescape") for s in segs for n in s[3]]
+        app = np.asarray([1 if s[5] else 0 for s in segs], dtype=np.uint8)
+        # row names are built by the writer from the contig prefixes and window positions
+        pre, rpre, rpos = [], [], []
+        for _, a, b, g, o, _ap in segs:
+            rpre.append(g.wpre[o: o + (b - a)].astype(np.uint32) + len(pre))
+            rpos.append(g.wpos[o: o + (b - a)].astype(np.uint64))
+            pre += g.prefixes
+        rpre = np.ascontiguousarray(np.concatenate(rpre), dtype=np.uint32)
+        rpos = np.ascontiguousarray(np.concatenate(rpos), dtype=np.uint64)
+        enc = [x.encode(errors="surrogateescape") for x in pre]
         arr = (ctypes.c_char_p * len(enc))(*enc)
-        N.check(N.lib().kf_write_kf_segments(len(segs), paths, row0.ctypes.data, app.ctypes.data, arr,
-                                             rows.ctypes.data, rows.shape[1], int(self.pseudocount), 1,
-                                             self.threads), "kf_write_kf_segments")
+        _tr("encode_names", t0, rows=int(rpos.size))
+        t0 = time.perf_counter()
+        N.check(N.lib().kf_write_kf_segments(len(segs), paths, row0.ctypes.data, app.ctypes.data, None, arr,
+                                             rpre.ctypes.data, rpos.ctypes.data, CHUNK_SZ, rows.ctypes.data,
+                                             rows.shape[1], int(self.pseudocount), 1, self.threads),
+                "kf_write_kf_segments")
+        _tr("format_write", t0, segs=len(segs))
 
     def drain(self) -> None:
         """Wait for every queued write."""

@@ -80,7 +80,7 @@ namespace kf {
 // SIMD issues its oldest wave first, so equal shares leave the older waves
 // waiting at every bucket barrier for the youngest.
 #ifndef KF_BK_RW
-#define KF_BK_RW 0
+#define KF_BK_RW 0x060B1114   // (20, 17, 11, 6): k=11 8.35 -> 8.17 ms, k=9 unchanged (profiles/r04/v6_lib_ab_k*_rw_dup.json)
 #endif
 constexpr uint32_t kBkSlots = KF_BK_LAG ? 2u : 1u;   // record / meta / roff slots per workgroup
 // Wave priority by age slot (tools/ A/B builds): bit 0 = phase 1, bit 1 = phase 2

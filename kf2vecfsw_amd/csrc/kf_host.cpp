@@ -1,8 +1,15 @@
 // kf_host.cpp -- host half of the kf2vec_gpu C-ABI (include/kf2vec_gpu.h):
 // bin tables / vocabulary, FASTA/FASTQ record index, byte-exact `.kf` formatting
 // and the parallel `.kf` writer.
+#include <fcntl.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
+#include <condition_variable>
+#include <memory>
 #include <charconv>
 #include <cstdarg>
 #include <cstdio>
@@ -267,6 +274,29 @@ const SmallText& small_text() {
 
 uint64_t kf_line_cap(size_t name_len, uint64_t nbins) { return name_len + 2 + nbins * 26; }
 
+// writev all of iov (bytes in total), resuming after short writes.
+bool write_all_v(int fd, struct iovec* iov, int cnt, uint64_t bytes) {
+    while (bytes) {
+        const ssize_t w = writev(fd, iov, cnt);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        bytes -= (uint64_t)w;
+        uint64_t d = (uint64_t)w;
+        while (cnt && d >= iov->iov_len) {
+            d -= iov->iov_len;
+            ++iov;
+            --cnt;
+        }
+        if (cnt) {
+            iov->iov_base = (char*)iov->iov_base + d;
+            iov->iov_len -= d;
+        }
+    }
+    return true;
+}
+
 // main.py:327-357
 uint64_t format_line(const char* name, const uint32_t* c, uint64_t nb, int pseudo, int raw, char* out) {
     char* p = out;
@@ -368,64 +398,136 @@ extern "C" int kf_write_kf_files(const char* dir, const char* const* names, int3
     return KF_OK;
 }
 
-// Row-granular parallel formatting of every row of every segment, then one
-// sequential write per segment file (segments in parallel, rows in order).
+// get_chunks' writer.  One pool of n_threads workers: a worker writes a segment
+// whose rows are all formatted (one writev stream per file, rows in order) and
+// otherwise formats the next row into its own arenas (no per-row allocation or
+// copy), so formatting and writing overlap.  Row i's name is names[i], or, with
+// names == NULL, prefixes[row_prefix[i]] + "<s+1>-<s+win_len>", s = row_start[i]
+// (the seqkit sliding window name of main.py:905-915).
 extern "C" int kf_write_kf_segments(int32_t n_seg, const char* const* paths, const int32_t* seg_row0,
-                                    const uint8_t* seg_append, const char* const* names, const uint32_t* counts,
-                                    uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
+                                    const uint8_t* seg_append, const char* const* names,
+                                    const char* const* prefixes, const uint32_t* row_prefix, const uint64_t* row_start,
+                                    uint32_t win_len, const uint32_t* counts, uint64_t nbins, int pseudocount,
+                                    int raw_cnt, int n_threads) {
     if (n_seg < 0 || (n_seg && (!paths || !seg_row0))) return kf_fail(KF_EINVAL, "null argument");
     if (n_seg == 0) return KF_OK;
     const int32_t n = seg_row0[n_seg];
     if (seg_row0[0] != 0 || n < 0) return kf_fail(KF_EINVAL, "seg_row0 must start at 0");
     for (int32_t g = 0; g < n_seg; ++g)
         if (seg_row0[g + 1] < seg_row0[g]) return kf_fail(KF_EINVAL, "seg_row0 must be non-decreasing");
-    if (n && (!names || !counts)) return kf_fail(KF_EINVAL, "null argument");
+    if (n && (!counts || (!names && (!prefixes || !row_prefix || !row_start))))
+        return kf_fail(KF_EINVAL, "null argument");
     if (n_threads < 1) n_threads = 1;
-    std::vector<std::vector<char>> rows((size_t)n);
-    std::atomic<int32_t> next{0};
-    auto fmt = [&]() {
-        std::vector<char> buf;
-        for (;;) {
-            const int32_t i = next.fetch_add(1);
-            if (i >= n) break;
-            buf.resize(kf_line_cap(strlen(names[i]), nbins));
-            const uint64_t w = format_line(names[i], counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt,
-                                           buf.data());
-            rows[i].assign(buf.data(), buf.data() + w);
-        }
-    };
-    std::atomic<int32_t> next_seg{0};
-    std::atomic<int> err{0};
+    std::vector<char*> rp((size_t)n, nullptr);
+    std::vector<uint64_t> rl((size_t)n, 0);
+    std::vector<int32_t> seg_of((size_t)n);
+    std::unique_ptr<std::atomic<int32_t>[]> left(new std::atomic<int32_t>[n_seg]);
+    std::vector<int32_t> ready;   // segments whose rows are all formatted, not yet claimed
+    for (int32_t g = 0; g < n_seg; ++g) {
+        left[g].store(seg_row0[g + 1] - seg_row0[g]);
+        for (int32_t i = seg_row0[g]; i < seg_row0[g + 1]; ++i) seg_of[i] = g;
+        if (seg_row0[g + 1] == seg_row0[g]) ready.push_back(g);
+    }
+    const int nw = std::min<int>(n_threads, std::max<int32_t>(n, n_seg));
+    std::vector<std::vector<std::unique_ptr<char[]>>> arenas((size_t)nw);
+    std::atomic<int32_t> next_row{0};
+    int32_t written = 0;
+    int err = 0;
     std::string errmsg;
     std::mutex mu;
-    auto wr = [&]() {
+    std::condition_variable cv;
+    auto write_seg = [&](int32_t g, std::vector<struct iovec>& iov) -> bool {
+        const int fd = open(paths[g], O_WRONLY | O_CREAT | ((seg_append && seg_append[g]) ? O_APPEND : O_TRUNC), 0666);
+        bool ok = fd >= 0;
+        for (int32_t i = seg_row0[g]; ok && i < seg_row0[g + 1];) {
+            iov.clear();
+            uint64_t bytes = 0;
+            for (; i < seg_row0[g + 1] && iov.size() < 512; ++i) {
+                iov.push_back({rp[i], (size_t)rl[i]});
+                bytes += rl[i];
+            }
+            ok = write_all_v(fd, iov.data(), (int)iov.size(), bytes);
+        }
+        if (fd >= 0) ok = (close(fd) == 0) && ok;
+        return ok;
+    };
+    auto work = [&](int t) {
+        constexpr uint64_t kArena = 16ull << 20;
+        char* pos = nullptr;
+        uint64_t left_b = 0;
+        std::vector<struct iovec> iov;
+        std::string nm;
         for (;;) {
-            const int32_t g = next_seg.fetch_add(1);
-            if (g >= n_seg || err.load()) break;
-            FILE* f = fopen(paths[g], (seg_append && seg_append[g]) ? "ab" : "wb");
-            bool ok = f != nullptr;
-            for (int32_t i = seg_row0[g]; ok && i < seg_row0[g + 1]; ++i)
-                ok = fwrite(rows[i].data(), 1, rows[i].size(), f) == rows[i].size();
-            if (f) ok = (fclose(f) == 0) && ok;
-            if (!ok) {
+            int32_t g = -1;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                for (;;) {
+                    if (err || written == n_seg) return;
+                    if (!ready.empty()) {
+                        g = ready.back();
+                        ready.pop_back();
+                        break;
+                    }
+                    if (next_row.load() < n) break;   // rows left to format
+                    cv.wait(lk);
+                }
+            }
+            if (g >= 0) {
+                const bool ok = write_seg(g, iov);
                 std::lock_guard<std::mutex> lk(mu);
-                if (!err.exchange(1)) errmsg = std::string("cannot write ") + paths[g];
+                if (!ok && !err) {
+                    err = 1;
+                    errmsg = std::string("cannot write ") + paths[g];
+                }
+                ++written;
+                cv.notify_all();
+                continue;
+            }
+            const int32_t i = next_row.fetch_add(1);
+            if (i >= n) continue;
+            const char* name = names ? names[i] : nullptr;
+            if (!name) {
+                char tmp[48];
+                const uint64_t s0 = row_start[i];
+                const int m = snprintf(tmp, sizeof tmp, "%llu-%llu", (unsigned long long)(s0 + 1),
+                                       (unsigned long long)(s0 + win_len));
+                nm.assign(prefixes[row_prefix[i]]);
+                nm.append(tmp, (size_t)m);
+                name = nm.c_str();
+            }
+            const uint64_t cap = kf_line_cap(strlen(name), nbins);
+            if (left_b < cap) {
+                const uint64_t sz = std::max(kArena, cap);
+                char* a = new (std::nothrow) char[sz];
+                if (!a) {
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (!err) { err = 1; errmsg = "out of host memory formatting rows"; }
+                    cv.notify_all();
+                    return;
+                }
+                arenas[t].emplace_back(a);
+                pos = a;
+                left_b = sz;
+            }
+            const uint64_t w = format_line(name, counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt, pos);
+            rp[i] = pos;
+            rl[i] = w;
+            pos += w;
+            left_b -= w;
+            if (left[seg_of[i]].fetch_sub(1) == 1) {   // the segment's last row: it can be written
+                std::lock_guard<std::mutex> lk(mu);
+                ready.push_back(seg_of[i]);
+                cv.notify_one();
             }
         }
     };
     {
         std::vector<std::thread> th;
-        for (int t = 1; t < std::min<int>(n_threads, std::max<int32_t>(n, 1)); ++t) th.emplace_back(fmt);
-        fmt();
+        for (int t = 1; t < nw; ++t) th.emplace_back(work, t);
+        work(0);
         for (auto& t : th) t.join();
     }
-    {
-        std::vector<std::thread> th;
-        for (int t = 1; t < std::min<int>(n_threads, n_seg); ++t) th.emplace_back(wr);
-        wr();
-        for (auto& t : th) t.join();
-    }
-    if (err.load()) return kf_fail(KF_EINVAL, "%s", errmsg.c_str());
+    if (err) return kf_fail(errmsg.rfind("out of", 0) == 0 ? KF_ERANGE : KF_EINVAL, "%s", errmsg.c_str());
     return KF_OK;
 }
 
@@ -433,7 +535,8 @@ extern "C" int kf_write_kf_rows(const char* path, const char* const* names, int3
                                 uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
     if (!path || (!names && n) || (!counts && n) || n < 0) return kf_fail(KF_EINVAL, "null argument");
     const int32_t row0[2] = {0, n};
-    return kf_write_kf_segments(1, &path, row0, nullptr, names, counts, nbins, pseudocount, raw_cnt, n_threads);
+    return kf_write_kf_segments(1, &path, row0, nullptr, names, nullptr, nullptr, nullptr, 0, counts, nbins, pseudocount,
+                                raw_cnt, n_threads);
 }
 
 // ------------------------------------------------------------------ synthetic layout

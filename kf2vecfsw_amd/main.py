@@ -488,6 +488,7 @@ def get_chunks(args) -> None:
     from . import chunks as CH
     from .counter import KmerCounter, pack_files
 
+    CH.TRACE = os.environ.get("KF_TRACE") == "1"
     since = time.time()
     if not os.path.exists(args.input_dir):
         print("No such directory '{}'".format(args.input_dir), file=sys.stderr)
@@ -518,19 +519,26 @@ def get_chunks(args) -> None:
     budget = int(float(getattr(args, "batch_gb", 1.0) or 1.0) * (1 << 30))
     # windows per count launch: the window bytes AND the count matrix (4 x bins
     # per window, 8 MiB at k=11) within the budget
-    max_windows = max(1, min(budget // CH.CHUNK_SZ, budget // (4 * counter.nbins)))
+    # and at most CH.LAUNCH_WINDOWS, so the writer formats one launch while the
+    # device counts and copies back the next
+    max_windows = max(1, min(budget // CH.CHUNK_SZ, budget // (4 * counter.nbins), CH.LAUNCH_WINDOWS))
     pipe = CH.ChunkPipeline(counter, device, max_windows, args.p, args.pseudocount)
     paths = [os.path.join(args.input_dir, f) for f in files_names]
-    # input batches of files (the processed sequence of a batch must stay below
-    # 4 GiB: kf_chunk_compact's offsets)
-    batches = _batches(paths, min(budget, 3 << 30))
+    # input batches of files: about a quarter of the input each, so that reading
+    # and preparing one batch overlaps writing the previous one, within the
+    # budget (and below 4 GiB of processed sequence: kf_chunk_compact's offsets)
+    total_in = sum(os.path.getsize(p) for p in paths)
+    batches = _batches(paths, min(budget, 3 << 30, max(total_in // 4, 16 << 20)))
     threads = max(1, int(args.p))
     files_pool = ThreadPoolExecutor(max_workers=threads)
     reader = ThreadPoolExecutor(max_workers=1)
 
     def read(idx):
-        return pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], fmt=N.KF_FMT_FASTA,
-                          pool=files_pool)
+        t0 = time.perf_counter()
+        hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], fmt=N.KF_FMT_FASTA,
+                        pool=files_pool)
+        CH._tr("read", t0, files=len(idx))
+        return hb
 
     def report(genomes):
         for gm in genomes:
@@ -546,7 +554,7 @@ def get_chunks(args) -> None:
             log.info(">>> Computing contig statistics. Sample: {}".format(gm.fname))          # :799
             if gm.excluded == "few":                                                          # :845-860
                 stamp("\n==> Excluded {}. {} chunks is too low. {} is required.".format(
-                    gm.fname, len(gm.names), CH.CHUNK_CNT_THR))
+                    gm.fname, gm.n_windows, CH.CHUNK_CNT_THR))
                 continue
             stamp("\n==> Done chunk processing for {}.".format(gm.fname))                    # :866
             # the reference runs get_frequencies on the genome's chunk directory here
@@ -559,12 +567,16 @@ def get_chunks(args) -> None:
     nxt = reader.submit(read, batches[0]) if batches else None
     prev = None   # (genomes, write futures) of the previous batch, logged once written
     for bi, idx in enumerate(batches):
+        t0 = time.perf_counter()
         hb = nxt.result()
+        CH._tr("wait_read", t0, batch=bi)
         if bi + 1 < len(batches):
             nxt = reader.submit(read, batches[bi + 1])
         genomes = [CH.Genome(files_names[i], samples_names[i]) for i in idx]
         d_seq = pipe.prepare(hb, genomes)
+        t0 = time.perf_counter()
         futs = pipe.count_and_write(d_seq, genomes, args.output_dir)
+        CH._tr("issue_counts", t0, launches=len(futs))
         del hb, d_seq
         if prev is not None:
             for f in prev[1]:
@@ -579,6 +591,10 @@ def get_chunks(args) -> None:
     reader.shutdown()
     files_pool.shutdown()
     stamp("\n==> Done getting chunks.")
+    if CH.TRACE:
+        import json
+        print(json.dumps({"kf_chunks_trace": CH.trace}), file=sys.stderr)
+        CH.trace.clear()
 
 
 def build_parser() -> argparse.ArgumentParser:

@@ -203,3 +203,61 @@ def test_features_handoff_equals_kf_text_round_trip(native, pseudo, raw):
         vals = format_kf("s", r, pseudo, raw).decode().rstrip("\n").split(",")[1:]
         exp = np.array([float(x) for x in vals]) * 10000.0
         assert np.array_equal(got[i], exp, equal_nan=True), i
+
+
+def test_write_kf_segments_append_and_arenas(native, oracle, tmp_path):
+    """kf_write_kf_segments (get_chunks' writer): several files at once, rows in
+    order, a segment appended to the file an earlier call started, raw counts
+    above and below the formatter's text table (1,024), and enough rows for the
+    per-thread 16 MiB formatting arenas to roll over."""
+    import ctypes
+    from kf2vecfsw_amd import _native as N
+    rng = np.random.default_rng(31)
+    nb = 8192
+    rows = rng.integers(0, 4, size=(700, nb)).astype(np.uint32)
+    rows[:, ::97] = rng.integers(1000, 5000, size=rows[:, ::97].shape)
+    names = [f"s.part_c{i % 3}.part_c{i % 3}_sliding__{i + 1}-{i + 10000}" for i in range(700)]
+    paths = [str(tmp_path / f"g{j}.kf") for j in range(3)]
+
+    def call(seg_paths, row0, app, lo, hi):
+        enc = [n.encode() for n in names[lo:hi]]
+        r0 = np.asarray(row0, np.int32)
+        ap = np.asarray(app, np.uint8)
+        sub = np.ascontiguousarray(rows[lo:hi])
+        rc = N.lib().kf_write_kf_segments(len(seg_paths), (ctypes.c_char_p * len(seg_paths))(*[p.encode() for p in seg_paths]),
+                                          r0.ctypes.data, ap.ctypes.data, (ctypes.c_char_p * len(enc))(*enc),
+                                          None, None, None, 0, sub.ctypes.data, nb, 0, 1, 3)
+        assert rc == 0, N.lib().kf_last_error()
+
+    # launch 1: g0 rows 0..299, g1 rows 300..399; launch 2: g1 continues (append) 400..549, g2 550..699
+    call(paths[:2], [0, 300, 400], [0, 0], 0, 400)
+    call(paths[1:], [0, 150, 300], [1, 0], 400, 700)
+    exp = ["".join(oracle.kf_line(names[i], rows[i], raw_cnt=True) for i in range(a, b))
+           for a, b in [(0, 300), (300, 550), (550, 700)]]
+    for p, e in zip(paths, exp):
+        assert open(p).read() == e
+    # a truncating segment replaces an earlier file
+    call(paths[:1], [0, 1], [0], 0, 1)
+    assert open(paths[0]).read() == oracle.kf_line(names[0], rows[0], raw_cnt=True)
+
+
+def test_write_kf_segments_generated_names(native, oracle, tmp_path):
+    """kf_write_kf_segments with names built by the writer from contig prefixes and
+    window positions (get_chunks' rows: "<sample>.part_<cid>.part_<cid>_sliding__<s+1>-<s+10000>")."""
+    import ctypes
+    from kf2vecfsw_amd import _native as N
+    from kf2vecfsw_amd import chunks as CH
+    rng = np.random.default_rng(32)
+    rows = rng.integers(0, 3, size=(40, 512)).astype(np.uint32)
+    pre = ["g.part_c1.part_c1_sliding__", "g.part_x y.part_x y_sliding__"]
+    rpre = np.asarray([0] * 25 + [1] * 15, np.uint32)
+    rpos = np.asarray(list(range(0, 25 * 9930, 9930)) + list(range(0, 15 * 9990, 9990)), np.uint64)
+    path = str(tmp_path / "g.kf")
+    r0 = np.asarray([0, 40], np.int32)
+    enc = [p.encode() for p in pre]
+    rc = N.lib().kf_write_kf_segments(1, (ctypes.c_char_p * 1)(path.encode()), r0.ctypes.data, None, None,
+                                      (ctypes.c_char_p * 2)(*enc), rpre.ctypes.data, rpos.ctypes.data, CH.CHUNK_SZ,
+                                      rows.ctypes.data, 512, 0, 1, 4)
+    assert rc == 0, N.lib().kf_last_error()
+    names = [pre[p] + "{}-{}".format(s + 1, s + CH.CHUNK_SZ) for p, s in zip(rpre.tolist(), rpos.tolist())]
+    assert open(path).read() == "".join(oracle.kf_line(n, r, raw_cnt=True) for n, r in zip(names, rows))

@@ -53,6 +53,7 @@ def main():
         open(os.path.join(d, "B%04d.fna" % g), "wb").write(_bacterial_like(rng, 5_000_000))
     sets["bacterial_like"] = d
     res = {}
+    traces = {}
     for name, inp in sets.items():
         walls = []
         for r in range(args.reps + 1):
@@ -60,8 +61,15 @@ def main():
             shutil.rmtree(out, ignore_errors=True)
             os.makedirs(out)
             t0 = time.perf_counter()
-            with contextlib.redirect_stdout(io.StringIO()):
+            os.environ["KF_TRACE"] = "1" if r == args.reps else "0"
+            err = io.StringIO()
+            with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(err):
                 M.main(["get_chunks", "-input_dir", inp, "-output_dir", out, "-k", "7", "-p", str(args.threads)])
+            for ln in err.getvalue().splitlines():
+                if ln.startswith('{"kf_chunks_trace"'):
+                    tr = json.loads(ln)["kf_chunks_trace"]
+                    t_first = min(e[1] for e in tr) if tr else 0
+                    traces[name] = [(e[0], round(e[1] - t_first, 2), round(e[2] - t_first, 2), e[3]) for e in tr]
             if r:   # the first run warms the runtime and the page cache
                 walls.append(time.perf_counter() - t0)
         rows = sum(open(os.path.join(out, f)).read().count("\n") for f in os.listdir(out) if f.endswith(".kf"))
@@ -80,6 +88,7 @@ def main():
                      "kf_bytes": kfb, "kf_GBps": round(kfb / w / 1e9, 2), "walls": [round(x, 4) for x in walls],
                      "reference_rows_match": ok}
     shutil.rmtree(args.dir, ignore_errors=True)
+    res["trace_last_run"] = traces
     print(json.dumps(res, indent=1))
 
 
