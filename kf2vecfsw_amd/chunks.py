@@ -272,27 +272,25 @@ class ChunkPipeline:
                     continue
                 segs.append((os.path.join(output_dir, "{}.kf".format(g.sample)), a - w0, b - w0, g,
                              a - int(row0[gi]), a > int(row0[gi])))
+            args = self._write_args(segs)   # built here: the writer thread only formats + writes
             if len(self.pending) >= 2:      # at most two launches queued for the writer
                 self.pending.pop(0).result()
-            futs.append(self.writer.submit(self._write, ev, host, segs))
+            futs.append(self.writer.submit(self._write, ev, host, args))
             self.pending.append(futs[-1])
             del counts
         return futs
 
-    def _write(self, ev, host: torch.Tensor, segs) -> None:
-        """Format + write one launch's rows (segments are consecutive row ranges)."""
+    def _write_args(self, segs):
+        """kf_write_kf_segments' arguments for one launch's segments (consecutive
+        row ranges): paths, row bounds, append flags and the row-name parts (the
+        writer builds the names from contig prefixes and window positions)."""
         import time
         t0 = time.perf_counter()
-        ev.synchronize()
-        _tr("wait_d2h", t0)
-        t0 = time.perf_counter()
         if not segs:
-            return
-        rows = host.numpy().view(np.uint32)
+            return None
         paths = (ctypes.c_char_p * len(segs))(*[os.fsencode(s[0]) for s in segs])
         row0 = np.asarray([0] + [s[2] for s in segs], dtype=np.int32)
         app = np.asarray([1 if s[5] else 0 for s in segs], dtype=np.uint8)
-        # row names are built by the writer from the contig prefixes and window positions
         pre, rpre, rpos = [], [], []
         for _, a, b, g, o, _ap in segs:
             rpre.append(g.wpre[o: o + (b - a)].astype(np.uint32) + len(pre))
@@ -303,12 +301,24 @@ class ChunkPipeline:
         enc = [x.encode(errors="surrogateescape") for x in pre]
         arr = (ctypes.c_char_p * len(enc))(*enc)
         _tr("encode_names", t0, rows=int(rpos.size))
+        return (len(segs), paths, row0, app, enc, arr, rpre, rpos)
+
+    def _write(self, ev, host: torch.Tensor, args) -> None:
+        """Format + write one launch's rows, once its counts are on the host."""
+        import time
         t0 = time.perf_counter()
-        N.check(N.lib().kf_write_kf_segments(len(segs), paths, row0.ctypes.data, app.ctypes.data, None, arr,
+        ev.synchronize()
+        _tr("wait_d2h", t0)
+        if args is None:
+            return
+        t0 = time.perf_counter()
+        n_seg, paths, row0, app, _enc, arr, rpre, rpos = args
+        rows = host.numpy().view(np.uint32)
+        N.check(N.lib().kf_write_kf_segments(n_seg, paths, row0.ctypes.data, app.ctypes.data, None, arr,
                                              rpre.ctypes.data, rpos.ctypes.data, CHUNK_SZ, rows.ctypes.data,
                                              rows.shape[1], int(self.pseudocount), 1, self.threads),
                 "kf_write_kf_segments")
-        _tr("format_write", t0, segs=len(segs))
+        _tr("format_write", t0, segs=n_seg)
 
     def drain(self) -> None:
         """Wait for every queued write."""

@@ -1,7 +1,9 @@
 // kf_host.cpp -- host half of the kf2vec_gpu C-ABI (include/kf2vec_gpu.h):
 // bin tables / vocabulary, FASTA/FASTQ record index, byte-exact `.kf` formatting
 // and the parallel `.kf` writer.
+#include <emmintrin.h>
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
@@ -249,8 +251,10 @@ inline char* fmt_u64(uint64_t v, char* p) {
 }
 
 // Small counts are most of a row (a 10 kbp get_chunks window has 8,192 columns
-// at k=7, nearly all 0-3): their text comes from a table built once.
-//   kSmallInt[c] = "c", kSmallHalf[c] = "c.5" (pseudocount), kSmallF[c] = "c.0"
+// at k=7, nearly all 0-3).  Single digits go eight columns at a time through SSE2
+// (one add per column: "d.0," is the little-endian word 0x2C302E30 + d); the rest
+// come from a table built once, each entry with its trailing comma:
+//   txt[0][c] = "c,", txt[1][c] = "c.5," (pseudocount), txt[2][c] = "c.0,"
 constexpr uint32_t kSmall = 1024;
 struct SmallText {
     char txt[3][kSmall][8];
@@ -262,6 +266,7 @@ struct SmallText {
                 char* e = fmt_u64(c, p);
                 if (m == 1) { *e++ = '.'; *e++ = '5'; }
                 if (m == 2) { *e++ = '.'; *e++ = '0'; }
+                *e++ = ',';
                 len[m][c] = (uint8_t)(e - p);
             }
         }
@@ -272,30 +277,60 @@ const SmallText& small_text() {
     return t;
 }
 
-uint64_t kf_line_cap(size_t name_len, uint64_t nbins) { return name_len + 2 + nbins * 26; }
-
-// writev all of iov (bytes in total), resuming after short writes.
-bool write_all_v(int fd, struct iovec* iov, int cnt, uint64_t bytes) {
-    while (bytes) {
-        const ssize_t w = writev(fd, iov, cnt);
-        if (w < 0) {
-            if (errno == EINTR) continue;
-            return false;
+// columns [0, n) of one raw row, each followed by ','; m as in SmallText.  Adds the
+// number of zero columns to *zeros.
+inline char* raw_columns(const uint32_t* c, uint64_t n, int m, char* p, uint64_t* zeros) {
+    const SmallText& T = small_text();
+    auto one = [&](uint32_t v) {
+        if (v < kSmall) {
+            memcpy(p, T.txt[m][v], 8);   // the row buffer has >= 26 B per column
+            p += T.len[m][v];
+        } else {
+            p = fmt_u64(v, p);
+            if (m == 1) { *p++ = '.'; *p++ = '5'; }
+            if (m == 2) { *p++ = '.'; *p++ = '0'; }
+            *p++ = ',';
         }
-        bytes -= (uint64_t)w;
-        uint64_t d = (uint64_t)w;
-        while (cnt && d >= iov->iov_len) {
-            d -= iov->iov_len;
-            ++iov;
-            --cnt;
+    };
+    const __m128i sgn = _mm_set1_epi32((int)0x80000000u);
+    const __m128i lim = _mm_set1_epi32((int)0x8000000Au);   // unsigned v < 10 as a signed compare
+    const __m128i w4 = _mm_set1_epi32(m == 1 ? 0x2C352E30 : 0x2C302E30);   // "0.5," / "0.0,"
+    const __m128i w2 = _mm_set1_epi16(0x2C30);                            // "0,"
+    const __m128i zero = _mm_setzero_si128();
+    uint64_t zs = 0, i = 0;
+    while (i + 8 <= n) {
+        __m128i z = _mm_setzero_si128();   // 32-bit lane counters, folded every 2^30 groups
+        const uint64_t end = std::min<uint64_t>(n & ~7ull, i + (8ull << 30));
+        for (; i < end; i += 8) {
+            const __m128i a = _mm_loadu_si128((const __m128i*)(c + i));
+            const __m128i b = _mm_loadu_si128((const __m128i*)(c + i + 4));
+            z = _mm_sub_epi32(z, _mm_add_epi32(_mm_cmpeq_epi32(a, zero), _mm_cmpeq_epi32(b, zero)));
+            const __m128i ok = _mm_and_si128(_mm_cmplt_epi32(_mm_xor_si128(a, sgn), lim),
+                                             _mm_cmplt_epi32(_mm_xor_si128(b, sgn), lim));
+            if (_mm_movemask_epi8(ok) != 0xFFFF) {
+                for (int j = 0; j < 8; ++j) one(c[i + j]);
+            } else if (m == 0) {
+                _mm_storeu_si128((__m128i*)p, _mm_add_epi16(_mm_packs_epi32(a, b), w2));
+                p += 16;
+            } else {
+                _mm_storeu_si128((__m128i*)p, _mm_add_epi32(a, w4));
+                _mm_storeu_si128((__m128i*)(p + 16), _mm_add_epi32(b, w4));
+                p += 32;
+            }
         }
-        if (cnt) {
-            iov->iov_base = (char*)iov->iov_base + d;
-            iov->iov_len -= d;
-        }
+        alignas(16) uint32_t zl[4];
+        _mm_store_si128((__m128i*)zl, z);
+        zs += (uint64_t)zl[0] + zl[1] + zl[2] + zl[3];
     }
-    return true;
+    for (; i < n; ++i) {
+        zs += c[i] == 0;
+        one(c[i]);
+    }
+    *zeros += zs;
+    return p;
 }
+
+uint64_t kf_line_cap(size_t name_len, uint64_t nbins) { return name_len + 2 + nbins * 26; }
 
 // main.py:327-357
 uint64_t format_line(const char* name, const uint32_t* c, uint64_t nb, int pseudo, int raw, char* out) {
@@ -304,37 +339,26 @@ uint64_t format_line(const char* name, const uint32_t* c, uint64_t nb, int pseud
     memcpy(p, name, nl);
     p += nl;
     *p++ = ',';
-    bool all_present = nb > 0;
-    double sum = 0.0;
-    for (uint64_t i = 0; i < nb; ++i) {
-        all_present &= c[i] > 0;
-        sum += (double)c[i];        // exact: integers < 2^53
-    }
-    if (pseudo) sum += 0.5 * (double)nb;   // exact: multiples of 0.5 < 2^53
     // Integer text ("54", not "54.0") in raw mode without pseudocount when the
     // merged column is not float64: every vocab k-mer is in the dump (pd.merge
     // keeps the dump's int64 column), or the dump is empty (an object column of
     // NaN, which fillna(0) fills with the int 0).  Pinned by
     // tests/golden/ref_postproc (dense_k3_raw, empty_k7_raw).
-    const bool int_text = raw && !pseudo && (all_present || sum == 0.0);
     if (raw) {
         // raw counts: "c" (integer text), "c.5" (pseudocount) or "c.0" -- what
-        // repr prints for an integral float64 below 1e16 (and c + 0.5 < 2^33)
-        const SmallText& T = small_text();
-        const int m = int_text ? 0 : (pseudo ? 1 : 2);
-        for (uint64_t i = 0; i < nb; ++i) {
-            if (i) *p++ = ',';
-            const uint32_t v = c[i];
-            if (v < kSmall) {
-                memcpy(p, T.txt[m][v], 8);   // the row buffer has >= 26 B per column
-                p += T.len[m][v];
-            } else {
-                p = fmt_u64(v, p);
-                if (m == 1) { *p++ = '.'; *p++ = '5'; }
-                if (m == 2) { *p++ = '.'; *p++ = '0'; }
-            }
-        }
+        // repr prints for an integral float64 below 1e16 (and c + 0.5 < 2^33).
+        // Written as float text first; the rare integer-text row (no zero column,
+        // or all zero) is written again.
+        uint64_t zeros = 0;
+        char* const p0 = p;
+        p = raw_columns(c, nb, pseudo ? 1 : 2, p0, &zeros);
+        if (!pseudo && (zeros == 0 || zeros == nb)) p = raw_columns(c, nb, 0, p0, &zeros);
+        if (nb) --p;   // the last column's ','
     } else {
+        uint64_t usum = 0;
+        for (uint64_t i = 0; i < nb; ++i) usum += c[i];
+        double sum = (double)usum;              // exact: integers < 2^53
+        if (pseudo) sum += 0.5 * (double)nb;   // exact: multiples of 0.5 < 2^53
         for (uint64_t i = 0; i < nb; ++i) {
             if (i) *p++ = ',';
             const double v = ((double)c[i] + (pseudo ? 0.5 : 0.0)) / sum;
@@ -398,12 +422,68 @@ extern "C" int kf_write_kf_files(const char* dir, const char* const* names, int3
     return KF_OK;
 }
 
-// get_chunks' writer.  One pool of n_threads workers: a worker writes a segment
-// whose rows are all formatted (one writev stream per file, rows in order) and
-// otherwise formats the next row into its own arenas (no per-row allocation or
-// copy), so formatting and writing overlap.  Row i's name is names[i], or, with
-// names == NULL, prefixes[row_prefix[i]] + "<s+1>-<s+win_len>", s = row_start[i]
-// (the seqkit sliding window name of main.py:905-915).
+// Row arenas, kept across calls: fresh blocks would page-fault (and be zeroed by
+// the kernel) on every launch's 130 MB of text.  Up to 1 GiB stays pooled.
+constexpr uint64_t kArena = 16ull << 20;
+struct ArenaPool {
+    std::mutex mu;
+    std::vector<char*> free;
+};
+ArenaPool& arena_pool() {
+    static ArenaPool* p = new ArenaPool;   // never destroyed: worker threads may outlive static teardown
+    return *p;
+}
+char* arena_get(uint64_t sz) {
+    if (sz == kArena) {
+        ArenaPool& P = arena_pool();
+        std::lock_guard<std::mutex> lk(P.mu);
+        if (!P.free.empty()) {
+            char* a = P.free.back();
+            P.free.pop_back();
+            return a;
+        }
+    }
+    const uint64_t al = 2ull << 20;
+    char* a = (char*)aligned_alloc(al, (sz + al - 1) / al * al);
+    if (a) madvise(a, sz, MADV_HUGEPAGE);
+    return a;
+}
+void arena_put(char* a, uint64_t sz) {
+    if (sz == kArena) {
+        ArenaPool& P = arena_pool();
+        std::lock_guard<std::mutex> lk(P.mu);
+        if (P.free.size() < 64) {
+            P.free.push_back(a);
+            return;
+        }
+    }
+    free(a);
+}
+
+// write all of buf at file offset off, resuming after short writes
+bool pwrite_all(int fd, const char* buf, uint64_t len, uint64_t off) {
+    while (len) {
+        const ssize_t w = pwrite(fd, buf, len, (off_t)off);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        buf += w;
+        len -= (uint64_t)w;
+        off += (uint64_t)w;
+    }
+    return true;
+}
+
+// get_chunks' writer.  The rows are cut into blocks (about 1 MB of text, never
+// across a segment); a pool of n_threads workers claims blocks in order, formats
+// each into its own arena and writes it with pwrite as soon as its file offset is
+// known, i.e. once every earlier block of the segment is formatted (the thread
+// that completes that prefix writes the blocks it releases).  So a file is written
+// while its later rows are still being formatted, and the tail after the last row
+// is one block.  Row i's name is names[i], or, with names == NULL,
+// prefixes[row_prefix[i]] + "<s+1>-<s+win_len>", s = row_start[i] (the seqkit
+// sliding window name of main.py:905-915).
 extern "C" int kf_write_kf_segments(int32_t n_seg, const char* const* paths, const int32_t* seg_row0,
                                     const uint8_t* seg_append, const char* const* names,
                                     const char* const* prefixes, const uint32_t* row_prefix, const uint64_t* row_start,
@@ -418,106 +498,137 @@ extern "C" int kf_write_kf_segments(int32_t n_seg, const char* const* paths, con
     if (n && (!counts || (!names && (!prefixes || !row_prefix || !row_start))))
         return kf_fail(KF_EINVAL, "null argument");
     if (n_threads < 1) n_threads = 1;
-    std::vector<char*> rp((size_t)n, nullptr);
-    std::vector<uint64_t> rl((size_t)n, 0);
-    std::vector<int32_t> seg_of((size_t)n);
-    std::unique_ptr<std::atomic<int32_t>[]> left(new std::atomic<int32_t>[n_seg]);
-    std::vector<int32_t> ready;   // segments whose rows are all formatted, not yet claimed
-    for (int32_t g = 0; g < n_seg; ++g) {
-        left[g].store(seg_row0[g + 1] - seg_row0[g]);
-        for (int32_t i = seg_row0[g]; i < seg_row0[g + 1]; ++i) seg_of[i] = g;
-        if (seg_row0[g + 1] == seg_row0[g]) ready.push_back(g);
-    }
-    const int nw = std::min<int>(n_threads, std::max<int32_t>(n, n_seg));
-    std::vector<std::vector<std::unique_ptr<char[]>>> arenas((size_t)nw);
-    std::atomic<int32_t> next_row{0};
-    int32_t written = 0;
-    int err = 0;
-    std::string errmsg;
-    std::mutex mu;
-    std::condition_variable cv;
-    auto write_seg = [&](int32_t g, std::vector<struct iovec>& iov) -> bool {
-        const int fd = open(paths[g], O_WRONLY | O_CREAT | ((seg_append && seg_append[g]) ? O_APPEND : O_TRUNC), 0666);
-        bool ok = fd >= 0;
-        for (int32_t i = seg_row0[g]; ok && i < seg_row0[g + 1];) {
-            iov.clear();
-            uint64_t bytes = 0;
-            for (; i < seg_row0[g + 1] && iov.size() < 512; ++i) {
-                iov.push_back({rp[i], (size_t)rl[i]});
-                bytes += rl[i];
-            }
-            ok = write_all_v(fd, iov.data(), (int)iov.size(), bytes);
-        }
-        if (fd >= 0) ok = (close(fd) == 0) && ok;
+    // files: opened up front (an empty segment still creates / truncates its file)
+    std::vector<int> fd((size_t)n_seg, -1);
+    std::vector<uint64_t> base((size_t)n_seg, 0);
+    auto close_all = [&]() {
+        bool ok = true;
+        for (int f : fd)
+            if (f >= 0) ok = (close(f) == 0) && ok;
         return ok;
     };
+    for (int32_t g = 0; g < n_seg; ++g) {
+        const bool app = seg_append && seg_append[g];
+        fd[g] = open(paths[g], O_WRONLY | O_CREAT | (app ? 0 : O_TRUNC), 0666);
+        const off_t end = fd[g] >= 0 && app ? lseek(fd[g], 0, SEEK_END) : 0;
+        if (fd[g] < 0 || end < 0) {
+            close_all();
+            return kf_fail(KF_EINVAL, "cannot write %s", paths[g]);
+        }
+        base[g] = (uint64_t)end;
+    }
+    // blocks
+    struct Block {
+        int32_t g, r0, r1;
+        bool done;
+        char* buf;
+        uint64_t len;
+    };
+    const uint64_t row_text = 4 * std::max<uint64_t>(nbins, 1) + 64;
+    const int32_t per = (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (1ull << 20) / row_text));
+    std::vector<Block> blk;
+    std::vector<int32_t> front((size_t)n_seg), blk_end((size_t)n_seg);
+    std::vector<std::vector<std::pair<int32_t, uint64_t>>> pending((size_t)n_seg);   // (block, file offset)
+    std::vector<uint8_t> writing((size_t)n_seg, 0);
+    for (int32_t g = 0; g < n_seg; ++g) {
+        front[g] = (int32_t)blk.size();
+        for (int32_t r = seg_row0[g]; r < seg_row0[g + 1]; r += per)
+            blk.push_back({g, r, std::min(r + per, seg_row0[g + 1]), false, nullptr, 0});
+        blk_end[g] = (int32_t)blk.size();
+    }
+    const int32_t nb = (int32_t)blk.size();
+    // claim order: every segment at the same relative pace, so concurrent workers
+    // hold different files (writes to one file serialise on its inode) and the
+    // segments finish together
+    std::vector<int32_t> order((size_t)nb);
+    {
+        std::vector<std::pair<double, int32_t>> key((size_t)nb);
+        for (int32_t g = 0, b0 = 0; g < n_seg; b0 = blk_end[g], ++g)
+            for (int32_t b = b0; b < blk_end[g]; ++b)
+                key[b] = {(b - b0 + 0.5) / (double)(blk_end[g] - b0), b};
+        std::sort(key.begin(), key.end());
+        for (int32_t j = 0; j < nb; ++j) order[j] = key[j].second;
+    }
+    const int nw = std::min<int>(n_threads, std::max<int32_t>(nb, 1));
+    std::vector<std::vector<std::pair<char*, uint64_t>>> arenas((size_t)nw);
+    std::atomic<int32_t> next{0};
+    std::atomic<int> err{0};
+    std::string errmsg;
+    std::mutex mu;
+    auto fail = [&](const std::string& m) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!err.exchange(1)) errmsg = m;
+    };
     auto work = [&](int t) {
-        constexpr uint64_t kArena = 16ull << 20;
         char* pos = nullptr;
         uint64_t left_b = 0;
-        std::vector<struct iovec> iov;
         std::string nm;
+        std::vector<std::pair<int32_t, uint64_t>> release;
         for (;;) {
-            int32_t g = -1;
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                for (;;) {
-                    if (err || written == n_seg) return;
-                    if (!ready.empty()) {
-                        g = ready.back();
-                        ready.pop_back();
-                        break;
-                    }
-                    if (next_row.load() < n) break;   // rows left to format
-                    cv.wait(lk);
-                }
-            }
-            if (g >= 0) {
-                const bool ok = write_seg(g, iov);
-                std::lock_guard<std::mutex> lk(mu);
-                if (!ok && !err) {
-                    err = 1;
-                    errmsg = std::string("cannot write ") + paths[g];
-                }
-                ++written;
-                cv.notify_all();
-                continue;
-            }
-            const int32_t i = next_row.fetch_add(1);
-            if (i >= n) continue;
-            const char* name = names ? names[i] : nullptr;
-            if (!name) {
-                char tmp[48];
-                const uint64_t s0 = row_start[i];
-                const int m = snprintf(tmp, sizeof tmp, "%llu-%llu", (unsigned long long)(s0 + 1),
-                                       (unsigned long long)(s0 + win_len));
-                nm.assign(prefixes[row_prefix[i]]);
-                nm.append(tmp, (size_t)m);
-                name = nm.c_str();
-            }
-            const uint64_t cap = kf_line_cap(strlen(name), nbins);
+            const int32_t j = next.fetch_add(1);
+            if (j >= nb || err.load()) return;
+            Block& B = blk[order[j]];
+            // the block's capacity: one arena holds the whole block
+            uint64_t cap = 0;
+            for (int32_t i = B.r0; i < B.r1; ++i)
+                cap += kf_line_cap(names ? strlen(names[i]) : strlen(prefixes[row_prefix[i]]) + 48, nbins);
             if (left_b < cap) {
                 const uint64_t sz = std::max(kArena, cap);
-                char* a = new (std::nothrow) char[sz];
+                char* a = arena_get(sz);
                 if (!a) {
-                    std::lock_guard<std::mutex> lk(mu);
-                    if (!err) { err = 1; errmsg = "out of host memory formatting rows"; }
-                    cv.notify_all();
+                    fail("out of host memory formatting rows");
                     return;
                 }
-                arenas[t].emplace_back(a);
+                arenas[t].emplace_back(a, sz);
                 pos = a;
                 left_b = sz;
             }
-            const uint64_t w = format_line(name, counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt, pos);
-            rp[i] = pos;
-            rl[i] = w;
-            pos += w;
-            left_b -= w;
-            if (left[seg_of[i]].fetch_sub(1) == 1) {   // the segment's last row: it can be written
+            char* const start = pos;
+            for (int32_t i = B.r0; i < B.r1; ++i) {
+                const char* name = names ? names[i] : nullptr;
+                if (!name) {
+                    char tmp[48];
+                    const uint64_t s0 = row_start[i];
+                    const int m = snprintf(tmp, sizeof tmp, "%llu-%llu", (unsigned long long)(s0 + 1),
+                                           (unsigned long long)(s0 + win_len));
+                    nm.assign(prefixes[row_prefix[i]]);
+                    nm.append(tmp, (size_t)m);
+                    name = nm.c_str();
+                }
+                pos += format_line(name, counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt, pos);
+            }
+            left_b -= (uint64_t)(pos - start);
+            const int32_t g = B.g;
+            release.clear();
+            {
                 std::lock_guard<std::mutex> lk(mu);
-                ready.push_back(seg_of[i]);
-                cv.notify_one();
+                B.buf = start;
+                B.len = (uint64_t)(pos - start);
+                B.done = true;
+                while (front[g] < blk_end[g] && blk[front[g]].done) {
+                    pending[g].emplace_back(front[g], base[g]);
+                    base[g] += blk[front[g]].len;
+                    ++front[g];
+                }
+                // one writer per file at a time: a busy file's blocks are written by
+                // the thread already writing it, this one goes back to formatting
+                if (writing[g] || pending[g].empty()) continue;
+                writing[g] = 1;
+                release.swap(pending[g]);
+            }
+            for (;;) {
+                for (auto& r : release)
+                    if (!pwrite_all(fd[g], blk[r.first].buf, blk[r.first].len, r.second)) {
+                        fail(std::string("cannot write ") + paths[g]);
+                        return;
+                    }
+                release.clear();
+                std::lock_guard<std::mutex> lk(mu);
+                if (pending[g].empty()) {
+                    writing[g] = 0;
+                    break;
+                }
+                release.swap(pending[g]);
             }
         }
     };
@@ -527,7 +638,13 @@ extern "C" int kf_write_kf_segments(int32_t n_seg, const char* const* paths, con
         work(0);
         for (auto& t : th) t.join();
     }
-    if (err) return kf_fail(errmsg.rfind("out of", 0) == 0 ? KF_ERANGE : KF_EINVAL, "%s", errmsg.c_str());
+    for (auto& v : arenas)
+        for (auto& a : v) arena_put(a.first, a.second);
+    if (!close_all() && !err.load()) {
+        err = 1;
+        errmsg = "cannot close an output file";
+    }
+    if (err.load()) return kf_fail(errmsg.rfind("out of", 0) == 0 ? KF_ERANGE : KF_EINVAL, "%s", errmsg.c_str());
     return KF_OK;
 }
 

@@ -75,11 +75,15 @@ def _pipeline_budget(paths: list[str], batch_gb) -> int:
     return int(min(max(total // parts, 16 << 20), 4 << 30))
 
 
-def _batches(paths: list[str], budget: int) -> list[list[int]]:
+def _batches(paths: list[str], budget: int, ramp: bool = False) -> list[list[int]]:
+    """Consecutive files in batches of at most `budget` bytes (a file larger than
+    that alone).  ramp: the first two batches get a quarter and a half of it, so a
+    pipeline's later stages start sooner."""
     out, cur, size = [], [], 0
     for i, p in enumerate(paths):
         s = os.path.getsize(p)
-        if cur and size + s > budget:
+        lim = budget >> max(0, 2 - len(out)) if ramp else budget
+        if cur and size + s > lim:
             out.append(cur)
             cur, size = [], 0
         cur.append(i)
@@ -524,11 +528,12 @@ def get_chunks(args) -> None:
     max_windows = max(1, min(budget // CH.CHUNK_SZ, budget // (4 * counter.nbins), CH.LAUNCH_WINDOWS))
     pipe = CH.ChunkPipeline(counter, device, max_windows, args.p, args.pseudocount)
     paths = [os.path.join(args.input_dir, f) for f in files_names]
-    # input batches of files: about a quarter of the input each, so that reading
-    # and preparing one batch overlaps writing the previous one, within the
-    # budget (and below 4 GiB of processed sequence: kf_chunk_compact's offsets)
+    # input batches of files: about a quarter of the input each (the first two
+    # smaller, so the writer starts sooner), so that reading and preparing one
+    # batch overlaps writing the previous one, within the budget (and below 4 GiB
+    # of processed sequence: kf_chunk_compact's offsets)
     total_in = sum(os.path.getsize(p) for p in paths)
-    batches = _batches(paths, min(budget, 3 << 30, max(total_in // 4, 16 << 20)))
+    batches = _batches(paths, min(budget, 3 << 30, max(total_in // 4, 16 << 20)), ramp=True)
     threads = max(1, int(args.p))
     files_pool = ThreadPoolExecutor(max_workers=threads)
     reader = ThreadPoolExecutor(max_workers=1)

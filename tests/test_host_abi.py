@@ -73,6 +73,13 @@ def test_format_kf_modes_match_oracle(native, oracle, pseudo, raw):
              rng.integers(1, 100, size=2080).astype(np.uint32),          # all bins present -> int dtype
              np.zeros(32, np.uint32), np.ones(1, np.uint32),
              (rng.pareto(1.0, size=8192) * 10).astype(np.uint32)]
+    # the writer's eight-column single-digit path: groups broken by 9/10/1023/1024/
+    # 2^31, ragged tails, all-present and all-zero rows of every length to 33
+    for n in range(0, 34):
+        c = rng.poisson(1.2, size=n).astype(np.uint32)
+        if n:
+            c[rng.integers(0, n)] = rng.choice([9, 10, 1023, 1024, 2 ** 31, 2 ** 32 - 1])
+        cases += [c, c + 1, np.zeros(n, np.uint32), np.full(n, 9, np.uint32)]
     for c in cases:
         assert format_kf("s", c, pseudo, raw).decode() == oracle.kf_line("s", c, pseudo, raw)
 
