@@ -48,7 +48,8 @@ extern "C" {
 #define KF_EFORMAT (-4)  /* unparseable input */
 
 #define KF_MIN_K 2
-#define KF_MAX_K 12      /* device kernels; the CLI accepts 3..11 */
+#define KF_MAX_K 12      /* dense device kernels; the CLI accepts 3..11 */
+#define KF_SPARSE_MAX_K 31  /* kf_sparse_count (get_kmers, main.py:81-82) */
 
 /* kf_count_batch flags */
 #define KF_ACCUMULATE 1u /* do not zero d_counts / d_totals first */
@@ -122,11 +123,30 @@ int kf_workspace_reserve(int k, int32_t max_genomes);
 
 /* Grid the count kernel will use on the current device for k (workgroups,
  * threads per workgroup, dynamic LDS bytes); for roofline accounting.
- * Kernel choice: k <= 6 K1 (k1_kernel), k = 7 the pair kernel K1x
- * (k1x_kernel<7>), k = 8 its single-pass form (k1x_kernel<8>), k >= 9 the
- * two-phase bucket kernels (bucket_kernel<k>).  No environment variable
- * changes the choice. */
+ * Kernel choice: k <= 7 the pair kernel K1x (k1x_kernel<k>: (k+1)-mer pairs
+ * plus single k-mers in LDS), k = 8 its single-pass form (k1x_kernel<8>),
+ * k >= 9 the two-phase bucket kernels (bucket_kernel<k>).  No environment
+ * variable changes the choice. */
 int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
+
+/* ---- get_kmers at any k = 2..31 (replaces `jellyfish count -m K -C` +
+ * `jellyfish dump -c -t` of main.py:133-160, which keep the PRESENT canonical
+ * k-mers only).  For every genome of a batch laid out as for kf_count_batch:
+ * its distinct canonical k-mers in ascending standard 2-bit code (A0 C1 G2 T3,
+ * first base most significant: lexicographic order of the k-mer strings, the
+ * order of the vocab files) and their counts.  Same input semantics as
+ * kf_count_batch.  Genome g's results are d_keys[goff[g] + i] and
+ * d_counts[goff[g] + i] for i < d_nuniq[g] (a genome has at most goff[g+1] -
+ * goff[g] distinct k-mers, so both arrays hold batch_bytes = goff[n] entries).
+ * The device sorts the windows' keys (segmented LSD radix sort of 2k bits) in
+ * d_work, which must hold kf_sparse_workspace_bytes(k, batch_bytes, n_genomes)
+ * bytes; d_keys is also used as sort scratch.  batch_bytes < 2^32.
+ * Asynchronous on `stream`, no allocation, no host synchronisation. */
+uint64_t kf_sparse_workspace_bytes(int k, uint64_t batch_bytes, int32_t n_genomes);
+int kf_sparse_count(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
+                    uint64_t batch_bytes, const uint64_t* d_excl, uint64_t n_excl, int k,
+                    void* d_work, uint64_t work_bytes, uint64_t* d_keys, uint32_t* d_counts,
+                    uint64_t* d_nuniq, void* stream);
 
 /* Hash of the sources this library was built from (csrc/ + this header, as
  * kf2vecfsw_amd/build.py computes it): 16 hex digits, with a "+<tag>" suffix for

@@ -21,6 +21,7 @@ KF_ERANGE = -3
 KF_EFORMAT = -4
 KF_MIN_K = 2
 KF_MAX_K = 12
+KF_SPARSE_MAX_K = 31
 KF_ACCUMULATE = 1
 KF_FMT_AUTO, KF_FMT_FASTA, KF_FMT_FASTQ = 0, 1, 2
 
@@ -52,6 +53,8 @@ SIGNATURES = {
                                     _vp, _vp, _u32, _vp, _u64, _int, _int, _int]),
     "kf_chunk_compact": (_int, [_vp, _u64, _vp, _i32, _vp, _vp, _vp, _u64, _vp]),
     "kf_chunk_gather": (_int, [_vp, _vp, _i32, _u32, _vp, _vp]),
+    "kf_sparse_workspace_bytes": (_u64, [_int, _u64, _i32]),
+    "kf_sparse_count": (_int, [_vp, _vp, _i32, _u64, _vp, _u64, _int, _vp, _u64, _vp, _vp, _vp, _vp]),
 }
 
 

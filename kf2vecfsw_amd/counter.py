@@ -246,6 +246,66 @@ class KmerCounter:
         return counts, totals
 
 
+class SparseCounter:
+    """Present canonical k-mers at any k = 2..31 (``kf_sparse_count``): what
+    get_kmers reads from ``jellyfish count -C -m k`` + ``dump -c -t``
+    (main.py:133-160) -- per genome, the distinct canonical k-mers as standard
+    2-bit codes (A0 C1 G2 T3, first base most significant; ascending = the
+    lexicographic order of the vocab files) and their counts."""
+
+    def __init__(self, k: int, device: torch.device | str = "cuda"):
+        if not (N.KF_MIN_K <= k <= N.KF_SPARSE_MAX_K):
+            raise ValueError(f"k={k} out of range [{N.KF_MIN_K}, {N.KF_SPARSE_MAX_K}]")
+        self.k = k
+        self.device = torch.device(device)
+        if self.device.type != "cuda" or not torch.cuda.is_available():
+            raise N.NativeError("SparseCounter needs a ROCm GPU (no CPU fallback)")
+        self._work = None
+
+    def workspace_bytes(self, batch_bytes: int, n: int) -> int:
+        return int(N.lib().kf_sparse_workspace_bytes(self.k, int(batch_bytes), int(n)))
+
+    def count(self, db: DeviceBatch, batch_bytes: int, stream: int | None = None):
+        """Enqueue the sparse count of a batch whose genomes end at batch_bytes
+        (= off[n]); returns (keys int64[batch_bytes] holding uint64 codes,
+        counts int32[batch_bytes] holding uint32, nuniq int64[n]) on the device:
+        genome g's k-mers are keys[off[g] : off[g] + nuniq[g]]."""
+        batch_bytes = int(batch_bytes)
+        need = self.workspace_bytes(batch_bytes, db.n)
+        if self._work is None or self._work.numel() < need:
+            self._work = None
+            self._work = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        keys = torch.empty(max(batch_bytes, 1), dtype=torch.int64, device=self.device)
+        counts = torch.empty(max(batch_bytes, 1), dtype=torch.int32, device=self.device)
+        nuniq = torch.zeros(max(db.n, 1), dtype=torch.int64, device=self.device)
+        s = _stream_ptr(self.device) if stream is None else stream
+        with torch.cuda.device(self.device):
+            N.check(N.lib().kf_sparse_count(
+                db.data.data_ptr(), db.off.data_ptr(), db.n, batch_bytes,
+                db.excl.data_ptr() if db.n_excl else None, db.n_excl, self.k,
+                self._work.data_ptr(), self._work.numel(), keys.data_ptr(), counts.data_ptr(),
+                nuniq.data_ptr(), s), "kf_sparse_count")
+        return keys, counts, nuniq[: db.n]
+
+    def to_host(self, keys: torch.Tensor, counts: torch.Tensor, nuniq: torch.Tensor,
+                off: np.ndarray) -> list[tuple[np.ndarray, np.ndarray]]:
+        """Per genome (keys uint64[m], counts uint32[m]) on the host: each genome's
+        slice is gathered on the device and the batch copied back once."""
+        nu = nuniq.cpu().numpy()
+        if nu.size == 0 or int(nu.sum()) == 0:
+            return [(np.zeros(0, np.uint64), np.zeros(0, np.uint32)) for _ in range(nu.size)]
+        idx = torch.cat([torch.arange(int(off[g]), int(off[g]) + int(nu[g]), device=keys.device)
+                         for g in range(nu.size)])
+        hk = keys[idx].cpu().numpy().view(np.uint64)
+        hc = counts[idx].cpu().numpy().view(np.uint32)
+        out, pos = [], 0
+        for g in range(nu.size):
+            m = int(nu[g])
+            out.append((hk[pos: pos + m], hc[pos: pos + m]))
+            pos += m
+        return out
+
+
 def counts_to_numpy(counts: torch.Tensor) -> np.ndarray:
     return counts.cpu().numpy().view(np.uint32)
 

@@ -1,0 +1,511 @@
+// kf_sparse.hip -- `get_kmers` at any k = 2..31 (reference kf2vec/main.py:112-176)
+// for MI355X (gfx950).
+//
+// The reference runs `jellyfish count -m K -C` + `jellyfish dump -c -t` per genome
+// and keeps the PRESENT canonical k-mers only (main.py:133-160); its parser
+// accepts k = 2..31 (main.py:81-82, 1006).  A dense 4^k/2-bin row stops being
+// possible past k ~ 13 (k = 31: 2^61 bins), so this path sorts instead of
+// histogramming:
+//   1. emit    one key per input byte: the canonical code of the window ending
+//              at that byte (standard 2-bit code A0 C1 G2 T3, canonical = the
+//              smaller of the code and its reverse complement, i.e. the
+//              lexicographically smaller string), or SENT (= 4^k - 1, the code of
+//              T..T, never canonical) where no window ends;
+//   2. sort    each genome's keys, a segmented LSD radix sort of 2k bits in
+//              ceil(2k/8) passes of <= 8-bit digits: per pass a tile histogram,
+//              a per-(genome, digit) scan over the genome's tiles and a stable
+//              scatter (ranks by wave ballot matching, the tile re-ordered in LDS
+//              so every digit's keys leave as one contiguous run);
+//   3. unique  run heads of the sorted keys compacted with their positions; a
+//              run's count is the distance to the next head.  SENT sorts last and
+//              is dropped.
+// Keys are u32 for k <= 16 (half the bytes of every pass) and u64 above.
+//
+// Semantics are those of the dense counter (kf_count_batch): '\n' is
+// transparent, any other non-ACGT byte (either case counts) breaks the window,
+// the excluded byte ranges (headers, FASTQ '+' / quality lines, from
+// kf_index_records) break it too, and a window never spans two genomes.
+//
+// Layout: genome g owns key slots [goff[g], goff[g+1]) in every buffer (a genome
+// has at most as many windows as bytes), cut into 2048-slot tiles; tile t of
+// the batch belongs to the genome g with tfirst[g] <= t < tfirst[g+1].
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kf_internal.h"
+
+namespace kf {
+namespace {
+
+constexpr int kSBlock = 256;                   // threads per workgroup (4 waves)
+constexpr uint32_t kSTile = 2048;              // key slots per tile
+constexpr int kSPer = kSTile / kSBlock;        // 8 slots per thread
+constexpr int kSWaves = kSBlock / 64;
+constexpr uint32_t kSWaveSpan = kSTile / kSWaves;   // 512 slots per wave
+
+// Standard 2-bit code of a byte: A0 C1 G2 T3 (either case), 4 = '\n', 5 = other.
+__device__ __forceinline__ uint32_t sp_code(uint8_t c) {
+    switch (c | 0x20) {
+    case 'a': return 0;
+    case 'c': return 1;
+    case 'g': return 2;
+    case 't': return 3;
+    default: return c == '\n' ? 4u : 5u;
+    }
+}
+
+// Genome of tile t (t < tfirst[n]): the last g with tfirst[g] <= t (empty
+// genomes share their tfirst with the next genome).
+__device__ __forceinline__ int tile_genome(const uint32_t* tfirst, int n, uint32_t t) {
+    int lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const int m = (lo + hi) >> 1;
+        if (tfirst[m] <= t) lo = m;
+        else hi = m;
+    }
+    return lo;
+}
+
+struct TileSpan {
+    uint32_t g, gs, ge, base, cnt;   // genome, its slot range, the tile's first slot and slot count
+};
+
+__device__ __forceinline__ bool tile_span(const uint64_t* goff, const uint32_t* tfirst, int n, uint32_t t,
+                                          TileSpan& ts) {
+    if (t >= tfirst[n]) return false;
+    ts.g = (uint32_t)tile_genome(tfirst, n, t);
+    ts.gs = (uint32_t)goff[ts.g];
+    ts.ge = (uint32_t)goff[ts.g + 1];
+    ts.base = ts.gs + (t - tfirst[ts.g]) * kSTile;
+    ts.cnt = min(kSTile, ts.ge - ts.base);
+    return true;
+}
+
+// Exclusive prefix of one value per thread over the 256-thread workgroup.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int x = 0; x < w; ++x) before += wsum[x];
+    __syncthreads();
+    return before + inc - v;
+}
+
+// Lanes of the wave (among `valid`) whose digit equals this lane's: one ballot
+// per digit bit.
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, int bits, uint64_t valid) {
+    uint64_t m = valid;
+    for (int b = 0; b < bits; ++b) {
+        const bool one = (d >> b) & 1u;
+        const uint64_t bb = __ballot(one);
+        m &= one ? bb : ~bb;
+    }
+    return m;
+}
+
+// ---- tiles: tfirst[g] = exclusive prefix of ceil(len_g / kSTile), tfirst[n] = total
+__global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, int n, uint32_t* tfirst) {
+    __shared__ uint32_t sh[1024];
+    const int t = threadIdx.x;
+    uint32_t carry = 0;
+    for (int base = 0; base < n; base += 1024) {
+        const int g = base + t;
+        const uint32_t v = g < n ? (uint32_t)((goff[g + 1] - goff[g] + kSTile - 1) / kSTile) : 0u;
+        sh[t] = v;
+        __syncthreads();
+        for (int d = 1; d < 1024; d <<= 1) {
+            const uint32_t o = t >= d ? sh[t - d] : 0u;
+            __syncthreads();
+            sh[t] += o;
+            __syncthreads();
+        }
+        if (g < n) tfirst[g] = carry + sh[t] - v;
+        carry += sh[1023];
+        __syncthreads();
+    }
+    if (t == 0) tfirst[n] = carry;
+}
+
+// ---- 1. emit: thread = 8 consecutive bytes; its k-1 bases of context come from
+// a walk back over the bytes before it (newlines skipped; a break, an excluded
+// range or the genome start ends the walk), then it rolls forward.
+template <typename KeyT>
+__global__ void __launch_bounds__(kSBlock) sp_emit_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
+                                                          const uint32_t* tfirst, int n, const uint64_t* excl,
+                                                          uint32_t n_excl, int k, KeyT* __restrict__ keys) {
+    TileSpan ts;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    const uint32_t q0 = threadIdx.x * kSPer;
+    if (q0 >= ts.cnt) return;
+    const uint32_t p0 = ts.base + q0, p1 = ts.base + min(q0 + kSPer, ts.cnt);
+    const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
+    const uint64_t kmask = (1ull << (2 * k)) - 1;
+    const int hi = 2 * k - 2;
+    uint32_t code[kSPer];
+    bool any = false;
+    for (int j = 0; j < kSPer; ++j) {
+        code[j] = p0 + j < p1 ? sp_code(bytes[p0 + j]) : 4u;
+        any |= code[j] < 4;
+    }
+    if (!any) {   // no base here: no window ends in these bytes (and no walk back over a newline run)
+        for (int j = 0; j < kSPer; ++j)
+            if (p0 + j < p1) keys[p0 + j] = sent;
+        return;
+    }
+    // first excluded range ending after p0
+    uint32_t ix = 0;
+    {
+        uint32_t lo = 0, h = n_excl;
+        while (lo < h) {
+            const uint32_t m = (lo + h) >> 1;
+            if (excl[2 * m + 1] <= p0) lo = m + 1;
+            else h = m;
+        }
+        ix = lo;
+    }
+    // context: up to k-1 bases before p0 (most recent in the low pair)
+    const uint64_t stop = ix > 0 ? excl[2 * ix - 1] : 0;   // end of the last excluded range before p0
+    const uint64_t floor_ = max((uint64_t)ts.gs, stop);
+    uint64_t back = 0;
+    int m = 0;
+    for (uint64_t q = p0; q > floor_ && m < k - 1;) {
+        const uint32_t c = sp_code(bytes[--q]);
+        if (c == 4) continue;
+        if (c == 5) break;
+        back |= (uint64_t)c << (2 * m);
+        ++m;
+    }
+    uint64_t fw = 0, rc = 0;
+    int len = 0;
+    for (int i = m - 1; i >= 0; --i) {
+        const uint32_t c = (uint32_t)(back >> (2 * i)) & 3u;
+        fw = ((fw << 2) | c) & kmask;
+        rc = (rc >> 2) | ((uint64_t)(3u - c) << hi);
+        ++len;
+    }
+    KeyT out[kSPer];
+    for (int j = 0; j < kSPer; ++j) {
+        const uint32_t p = p0 + j;
+        KeyT key = sent;
+        if (p < p1) {
+            while (ix < n_excl && excl[2 * ix + 1] <= p) ++ix;
+            const bool ex = ix < n_excl && excl[2 * ix] <= p;
+            const uint32_t c = ex ? 5u : code[j];
+            if (c == 5) {
+                len = 0;
+            } else if (c < 4) {
+                fw = ((fw << 2) | c) & kmask;
+                rc = (rc >> 2) | ((uint64_t)(3u - c) << hi);
+                if (++len >= k) key = (KeyT)(fw < rc ? fw : rc);
+            }
+        }
+        out[j] = key;
+    }
+    for (int j = 0; j < kSPer; ++j)
+        if (p0 + j < p1) keys[p0 + j] = out[j];
+}
+
+// ---- 2a. per-tile digit histogram (one row per digit: hist[d * hstride + t])
+template <typename KeyT>
+__global__ void __launch_bounds__(kSBlock) sp_hist_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
+                                                          const uint32_t* tfirst, int n, int shift, int bits,
+                                                          uint32_t* hist, uint32_t hstride) {
+    __shared__ uint32_t wc[kSWaves][256];
+    TileSpan ts;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int i = tid; i < kSWaves * 256; i += kSBlock) (&wc[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t dmask = (1u << bits) - 1u;
+    for (int it = 0; it < kSPer; ++it) {
+        const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+        const bool v = li < ts.cnt;
+        const uint32_t d = v ? (uint32_t)(keys[ts.base + li] >> shift) & dmask : 0u;
+        const uint64_t m = match_digit(d, bits, __ballot(v));
+        if (v && __popcll(m & ((1ull << lane) - 1)) == 0) wc[w][d] += (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (tid <= (int)dmask) hist[(uint64_t)tid * hstride + blockIdx.x] = wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
+}
+
+// ---- 2b. workgroup (g, d): exclusive scan of hist[d][tiles of g] in place;
+// gtot[g * 256 + d] = the genome's count of digit d
+__global__ void __launch_bounds__(kSBlock) sp_scan_kernel(uint32_t* hist, uint32_t hstride, const uint32_t* tfirst,
+                                                          uint32_t* gtot) {
+    __shared__ uint32_t wsum[kSWaves];
+    __shared__ uint32_t tot;
+    const uint32_t g = blockIdx.x, d = blockIdx.y;
+    uint32_t* row = hist + (uint64_t)d * hstride;
+    const uint32_t t0 = tfirst[g], t1 = tfirst[g + 1];
+    uint32_t carry = 0;
+    for (uint32_t base = t0; base < t1; base += kSBlock) {
+        const uint32_t t = base + threadIdx.x;
+        const uint32_t v = t < t1 ? row[t] : 0u;
+        const uint32_t ex = block_excl_scan(v, wsum);
+        if (t < t1) row[t] = carry + ex;
+        if (threadIdx.x == kSBlock - 1) tot = ex + v;   // the chunk's total
+        __syncthreads();
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) gtot[g * 256 + d] = carry;
+}
+
+// ---- 2c. stable scatter of one tile by digit
+template <typename KeyT>
+__global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restrict__ in, KeyT* __restrict__ out,
+                                                             const uint64_t* goff, const uint32_t* tfirst, int n,
+                                                             int shift, int bits, const uint32_t* hist,
+                                                             uint32_t hstride, const uint32_t* gtot) {
+    __shared__ uint32_t wc[kSWaves][256];   // per wave: digit counts, then the wave's base inside the digit
+    __shared__ uint32_t lbase[256];         // tile-local start of each digit
+    __shared__ uint32_t gdst[256];          // global slot of the digit's first key in this tile, minus lbase
+    __shared__ uint32_t wsum[kSWaves];
+    __shared__ KeyT stage[kSTile];
+    TileSpan ts;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int i = tid; i < kSWaves * 256; i += kSBlock) (&wc[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t dmask = (1u << bits) - 1u;
+    const uint64_t lt = (1ull << lane) - 1;
+    KeyT key[kSPer];
+    uint32_t rank[kSPer];
+    for (int it = 0; it < kSPer; ++it) {
+        const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+        const bool v = li < ts.cnt;
+        const KeyT x = v ? in[ts.base + li] : (KeyT)0;
+        const uint32_t d = (uint32_t)(x >> shift) & dmask;
+        const uint64_t m = match_digit(d, bits, __ballot(v));
+        const uint32_t r = (uint32_t)__popcll(m & lt);
+        const uint32_t prior = wc[w][d];
+        if (v && r == 0) wc[w][d] = prior + (uint32_t)__popcll(m);
+        key[it] = x;
+        rank[it] = prior + r;
+    }
+    __syncthreads();
+    {
+        const int d = tid;   // one digit per thread (bits <= 8)
+        const uint32_t c0 = wc[0][d], c1 = wc[1][d], c2 = wc[2][d], c3 = wc[3][d];
+        const bool live = d <= (int)dmask;
+        const uint32_t tot = c0 + c1 + c2 + c3;
+        const uint32_t gt = live ? gtot[ts.g * 256 + d] : 0u;
+        const uint32_t lb = block_excl_scan(tot, wsum);
+        const uint32_t gb = block_excl_scan(gt, wsum);
+        wc[0][d] = 0;
+        wc[1][d] = c0;
+        wc[2][d] = c0 + c1;
+        wc[3][d] = c0 + c1 + c2;
+        lbase[d] = lb;
+        gdst[d] = live ? ts.gs + gb + hist[(uint64_t)d * hstride + blockIdx.x] - lb : 0u;
+    }
+    __syncthreads();
+    for (int it = 0; it < kSPer; ++it) {
+        const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+        if (li < ts.cnt) {
+            const uint32_t d = (uint32_t)(key[it] >> shift) & dmask;
+            stage[lbase[d] + wc[w][d] + rank[it]] = key[it];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < ts.cnt; i += kSBlock) {
+        const KeyT x = stage[i];
+        out[gdst[(uint32_t)(x >> shift) & dmask] + i] = x;
+    }
+}
+
+// ---- 3a. run heads per tile (into hist row 0)
+template <typename KeyT>
+__device__ __forceinline__ bool is_head(const KeyT* keys, uint32_t p, uint32_t gs) {
+    return p == gs || keys[p] != keys[p - 1];
+}
+
+template <typename KeyT>
+__global__ void __launch_bounds__(kSBlock) sp_heads_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
+                                                           const uint32_t* tfirst, int n, uint32_t* heads) {
+    __shared__ uint32_t wsum[kSWaves];
+    TileSpan ts;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    uint32_t c = 0;
+    for (uint32_t i = threadIdx.x; i < ts.cnt; i += kSBlock) c += is_head(keys, ts.base + i, ts.gs) ? 1u : 0u;
+    for (int d = 32; d >= 1; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) heads[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// ---- 3b. heads -> unique keys and their first slots (genome-relative)
+template <typename KeyT>
+__global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
+                                                            const uint32_t* tfirst, int n, const uint32_t* heads,
+                                                            uint64_t* __restrict__ ukeys, uint32_t* __restrict__ upos) {
+    __shared__ uint32_t wsum[kSWaves];
+    TileSpan ts;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t lt = (1ull << lane) - 1;
+    uint32_t hm = 0, mine = 0;   // head flags of this lane's slots
+    for (int it = 0; it < kSPer; ++it) {
+        const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+        const bool h = li < ts.cnt && is_head(keys, ts.base + li, ts.gs);
+        hm |= (h ? 1u : 0u) << it;
+        mine += (uint32_t)__popcll(__ballot(h));
+    }
+    if (lane == 0) wsum[w] = mine;
+    __syncthreads();
+    uint32_t u = heads[blockIdx.x];
+    for (int x = 0; x < w; ++x) u += wsum[x];
+    for (int it = 0; it < kSPer; ++it) {
+        const bool h = (hm >> it) & 1u;
+        const uint64_t b = __ballot(h);
+        if (h) {
+            const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+            const uint32_t j = u + (uint32_t)__popcll(b & lt);
+            ukeys[ts.gs + j] = (uint64_t)keys[ts.base + li];
+            upos[ts.gs + j] = ts.base + li - ts.gs;
+        }
+        u += (uint32_t)__popcll(b);
+    }
+}
+
+// ---- 3c. counts = distance to the next head; tiles index unique slots here
+__global__ void __launch_bounds__(kSBlock) sp_counts_kernel(const uint64_t* goff, const uint32_t* tfirst, int n,
+                                                            const uint32_t* nfull, const uint32_t* upos,
+                                                            uint32_t* __restrict__ counts) {
+    TileSpan ts;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    const uint32_t nf = nfull[ts.g * 256];
+    const uint32_t len = ts.ge - ts.gs;
+    for (uint32_t i = threadIdx.x; i < ts.cnt; i += kSBlock) {
+        const uint32_t u = ts.base + i - ts.gs;
+        if (u >= nf) break;
+        const uint32_t nxt = u + 1 < nf ? upos[ts.gs + u + 1] : len;
+        counts[ts.gs + u] = nxt - upos[ts.gs + u];
+    }
+}
+
+// ---- 3d. distinct k-mers per genome (SENT dropped)
+template <typename KeyT>
+__global__ void __launch_bounds__(256) sp_nuniq_kernel(const KeyT* keys, const uint64_t* goff, int n,
+                                                       const uint32_t* nfull, KeyT sent, uint64_t* nuniq) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    uint32_t nf = nfull[g * 256];
+    const uint64_t ge = goff[g + 1];
+    if (nf > 0 && keys[ge - 1] == sent) --nf;
+    nuniq[g] = nf;
+}
+
+// Workspace carve-up (byte offsets, 256-aligned).
+struct SpLayout {
+    uint64_t tfirst, keys, hist, gtot, upos, total;
+    uint32_t hstride;
+};
+
+uint64_t al256(uint64_t x) { return (x + 255) & ~255ull; }
+
+SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
+    SpLayout L;
+    const uint64_t ks = k <= 16 ? 4 : 8;
+    L.hstride = (uint32_t)(batch_bytes / kSTile + (uint64_t)n + 1);
+    uint64_t o = 0;
+    L.tfirst = o;
+    o = al256(o + 4ull * ((uint64_t)n + 1));
+    L.keys = o;
+    o = al256(o + ks * batch_bytes);
+    L.hist = o;
+    o = al256(o + 4ull * 256 * L.hstride);
+    L.gtot = o;
+    o = al256(o + 4ull * 256 * (uint64_t)n);
+    L.upos = o;
+    o = al256(o + 4ull * batch_bytes);
+    L.total = o;
+    return L;
+}
+
+template <typename KeyT>
+int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t batch_bytes, const uint64_t* d_excl,
+           uint64_t n_excl, int k, uint8_t* work, const SpLayout& L, uint64_t* d_keys, uint32_t* d_counts,
+           uint64_t* d_nuniq, hipStream_t s) {
+    uint32_t* tfirst = (uint32_t*)(work + L.tfirst);
+    KeyT* kw = (KeyT*)(work + L.keys);     // the sorted keys end here
+    KeyT* ka = (KeyT*)d_keys;              // d_keys doubles as the other sort buffer
+    uint32_t* hist = (uint32_t*)(work + L.hist);
+    uint32_t* gtot = (uint32_t*)(work + L.gtot);
+    uint32_t* upos = (uint32_t*)(work + L.upos);
+    const uint32_t grid = L.hstride;       // >= the batch's tile count
+    const int bits_total = 2 * k;
+    const int passes = (bits_total + 7) / 8;
+    const int bits = (bits_total + passes - 1) / passes;
+    hipLaunchKernelGGL(sp_tiles_kernel, dim3(1), dim3(1024), 0, s, d_goff, n, tfirst);
+    // the last pass must write kw: start in kw for an even number of passes
+    KeyT* src = (passes % 2 == 0) ? kw : ka;
+    KeyT* dst = (passes % 2 == 0) ? ka : kw;
+    hipLaunchKernelGGL(sp_emit_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, d_bytes, d_goff, tfirst, n, d_excl,
+                       (uint32_t)n_excl, k, src);
+    for (int p = 0; p < passes; ++p) {
+        const int shift = p * bits;
+        const int b = min(bits, bits_total - shift);
+        hipLaunchKernelGGL(sp_hist_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, src, d_goff, tfirst, n, shift, b,
+                           hist, L.hstride);
+        hipLaunchKernelGGL(sp_scan_kernel, dim3((uint32_t)n, 1u << b), dim3(kSBlock), 0, s, hist, L.hstride, tfirst,
+                           gtot);
+        hipLaunchKernelGGL(sp_scatter_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, src, dst, d_goff, tfirst, n,
+                           shift, b, hist, L.hstride, gtot);
+        KeyT* t = src;
+        src = dst;
+        dst = t;
+    }
+    // src == kw: sorted
+    hipLaunchKernelGGL(sp_heads_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, kw, d_goff, tfirst, n, hist);
+    hipLaunchKernelGGL(sp_scan_kernel, dim3((uint32_t)n, 1), dim3(kSBlock), 0, s, hist, L.hstride, tfirst, gtot);
+    hipLaunchKernelGGL(sp_unique_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, kw, d_goff, tfirst, n, hist, d_keys,
+                       upos);
+    hipLaunchKernelGGL(sp_counts_kernel, dim3(grid), dim3(kSBlock), 0, s, d_goff, tfirst, n, gtot, upos, d_counts);
+    const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
+    hipLaunchKernelGGL(sp_nuniq_kernel<KeyT>, dim3((n + 255) / 256), dim3(256), 0, s, kw, d_goff, n, gtot, sent,
+                       d_nuniq);
+    return KF_OK;
+}
+
+}  // namespace
+}  // namespace kf
+
+using namespace kf;
+
+extern "C" uint64_t kf_sparse_workspace_bytes(int k, uint64_t batch_bytes, int32_t n_genomes) {
+    if (k < 2 || k > KF_SPARSE_MAX_K || n_genomes < 0) return 0;
+    return sp_layout(k, batch_bytes, n_genomes).total;
+}
+
+extern "C" int kf_sparse_count(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
+                               uint64_t batch_bytes, const uint64_t* d_excl, uint64_t n_excl, int k, void* d_work,
+                               uint64_t work_bytes, uint64_t* d_keys, uint32_t* d_counts, uint64_t* d_nuniq,
+                               void* stream) {
+    if (k < 2 || k > KF_SPARSE_MAX_K) return kf_fail(KF_EINVAL, "k=%d out of range [2, %d]", k, KF_SPARSE_MAX_K);
+    if (n_genomes < 0) return kf_fail(KF_EINVAL, "n_genomes < 0");
+    if (n_genomes == 0) return KF_OK;
+    if (batch_bytes >= (1ull << 32))
+        return kf_fail(KF_EINVAL, "batch of %llu bytes: at most 4 GiB - 1 per call", (unsigned long long)batch_bytes);
+    if (n_excl >= (1ull << 31)) return kf_fail(KF_EINVAL, "too many excluded ranges");
+    if (!d_bytes || !d_goff || (n_excl && !d_excl) || !d_work || !d_keys || !d_counts || !d_nuniq)
+        return kf_fail(KF_EINVAL, "null device pointer");
+    const SpLayout L = sp_layout(k, batch_bytes, n_genomes);
+    if (work_bytes < L.total)
+        return kf_fail(KF_ERANGE, "workspace needs %llu bytes (kf_sparse_workspace_bytes)",
+                       (unsigned long long)L.total);
+    hipStream_t s = (hipStream_t)stream;
+    const int rc = k <= 16 ? sp_run<uint32_t>(d_bytes, d_goff, n_genomes, batch_bytes, d_excl, n_excl, k,
+                                              (uint8_t*)d_work, L, d_keys, d_counts, d_nuniq, s)
+                           : sp_run<uint64_t>(d_bytes, d_goff, n_genomes, batch_bytes, d_excl, n_excl, k,
+                                              (uint8_t*)d_work, L, d_keys, d_counts, d_nuniq, s);
+    if (rc != KF_OK) return rc;
+    if (hipGetLastError() != hipSuccess) return kf_fail(KF_EHIP, "sparse count launch failed");
+    return KF_OK;
+}

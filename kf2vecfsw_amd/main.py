@@ -434,12 +434,31 @@ def kmers_matrix(counts: np.ndarray, k: int) -> np.ndarray:
     return np.column_stack((vocab_digits(k)[nz].astype(np.float32), norm))
 
 
+_STD_TO_DIGIT = np.array([0, 2, 3, 1], dtype=np.uint8)   # standard code A0 C1 G2 T3 -> get_kmers digit
+
+
+def sparse_kmers_matrix(keys: np.ndarray, counts: np.ndarray, k: int) -> np.ndarray:
+    """kmers_matrix for the sparse counter (k up to 31): keys are the present
+    canonical k-mers as ascending standard 2-bit codes, so the rows come in the
+    same (lexicographic) order as kmers_matrix's vocab order."""
+    if keys.size == 0:
+        return np.zeros((0, k + 1), dtype=np.float32)
+    shifts = (2 * np.arange(k - 1, -1, -1, dtype=np.uint64))
+    digits = _STD_TO_DIGIT[((keys[:, None] >> shifts[None, :]) & np.uint64(3)).astype(np.intp)]
+    c = counts.astype(np.float32)
+    norm = c / np.sum(c)                                   # main.py:169
+    return np.column_stack((digits.astype(np.float32), norm))
+
+
 def get_kmers(args) -> None:
-    """kf2vec/main.py:112-184 on the GPU (all *.fna of input_dir in one batch)."""
+    """kf2vec/main.py:112-184 on the GPU (the *.fna of input_dir in batches).
+    k <= 12: the dense counter's rows, non-zero bins kept; k = 13..31 (the rest
+    of the reference's 2..31): the sparse counter (device radix sort of every
+    window's canonical code, kf_sparse_count)."""
     import glob
 
     import torch
-    from .counter import KmerCounter, counts_to_numpy, pack_files, to_device
+    from .counter import KmerCounter, SparseCounter, counts_to_numpy, pack_files, to_device
 
     if not os.path.exists(args.output_dir):             # main.py:121-122
         os.makedirs(args.output_dir)
@@ -447,16 +466,25 @@ def get_kmers(args) -> None:
     if not fasta_files:
         return
     device = torch.device(getattr(args, "device", None) or "cuda")
-    counter = KmerCounter(args.k, device)
+    sparse = args.k > N.KF_MAX_K
+    counter = SparseCounter(args.k, device) if sparse else KmerCounter(args.k, device)
     budget = int(float(getattr(args, "batch_gb", 4.0) or 4.0) * (1 << 30))
+    if sparse:   # ~25 device bytes per input byte; offsets are 32-bit
+        budget = min(budget, 1 << 30)
     for idx in _batches(fasta_files, budget):
         paths = [fasta_files[i] for i in idx]
         names = [os.path.basename(p).replace(".fna", "") for p in paths]   # main.py:127
-        counts, _ = counter.count(to_device(pack_files(paths, names), device))
-        c = counts_to_numpy(counts)
+        hb = pack_files(paths, names)
+        if sparse:
+            keys, cnts, nu = counter.count(to_device(hb, device), int(hb.off[-1]))
+            per = counter.to_host(keys, cnts, nu, hb.off)
+            del keys, cnts, nu
+        else:
+            counts, _ = counter.count(to_device(hb, device))
+            c = counts_to_numpy(counts)
         for j, base_name in enumerate(names):
             print(f"--- Processing {base_name} ---")
-            m = kmers_matrix(c[j], args.k)
+            m = sparse_kmers_matrix(per[j][0], per[j][1], args.k) if sparse else kmers_matrix(c[j], args.k)
             if m.shape[0] == 0:
                 print(f"Warning: No valid ATCG k-mers found in {base_name}")
                 continue
@@ -636,8 +664,9 @@ def build_parser() -> argparse.ArgumentParser:
     pk = sub.add_parser("get_kmers", description="Extract kmers and frequencies from FASTA files")
     pk.add_argument("-input_dir", help="Directory of input genomes or assemblies (dir of .fna files)")
     pk.add_argument("-output_dir", help="Directory for k-mer outputs (.npy files)")
-    pk.add_argument("-k", type=int, choices=list(range(N.KF_MIN_K, N.KF_MAX_K + 1)), default=default_k_len,
-                    help="K-mer length. Default: {}".format(default_k_len), metavar="K")
+    pk.add_argument("-k", type=int, choices=list(range(min_k_len, max_k_len + 1)), default=default_k_len,
+                    help="K-mer length [{}-{}]. Default: {}".format(min_k_len, max_k_len, default_k_len),
+                    metavar="K")
     pk.add_argument("-batch_gb", type=float, default=4.0, help="Input bytes per device batch (GiB)")
     pk.add_argument("-device", default=None, help="torch device (default: cuda)")
     pk.set_defaults(func=get_kmers)

@@ -55,6 +55,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_synth_header_len.restype = u64
         L.oracle_synth_header_len.argtypes = [ctypes.c_int64]
         L.oracle_synth_genome.argtypes = [ctypes.c_int64, u64, u64, i32, u64, vp, u64]
+        L.oracle_sparse_count.argtypes = [vp, u64, i32, i32, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -243,6 +244,27 @@ def kmers_matrix_from_dump(dump_lines: list[tuple[str, int]], k: int) -> np.ndar
     counts_array = np.array(counts, dtype=np.float32)              # :166
     normalized = counts_array / np.sum(counts_array)               # :169
     return np.column_stack((kmer_matrix, normalized))             # :172
+
+
+def sparse_count(data: bytes | np.ndarray, k: int, fmt: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Present canonical k-mers of one genome at any k <= 31 (what `jellyfish
+    count -C` + `dump -c` give get_kmers, main.py:133-160), ascending by standard
+    2-bit code (lexicographic), and their counts (kmer_oracle.c oracle_sparse_count)."""
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    keys = np.zeros(max(a.size, 1), dtype=np.uint64)
+    cnt = np.zeros(max(a.size, 1), dtype=np.uint32)
+    n = ctypes.c_uint64(0)
+    assert lib().oracle_sparse_count(_ptr(a), a.size, k, fmt, _ptr(keys), _ptr(cnt), ctypes.byref(n)) == 0
+    return keys[: n.value].copy(), cnt[: n.value].copy()
+
+
+def std_code_text(keys: np.ndarray, k: int) -> list[str]:
+    """k-mer strings of standard 2-bit codes (A0 C1 G2 T3, first base most significant)."""
+    keys = np.asarray(keys, dtype=np.uint64)
+    sh = 2 * np.arange(k - 1, -1, -1, dtype=np.uint64)
+    chars = np.frombuffer(b"ACGT", np.uint8)[((keys[:, None] >> sh[None, :]) & np.uint64(3)).astype(np.intp)]
+    return [r.tobytes().decode() for r in chars]
 
 
 def dump_lines(counts: np.ndarray, k: int) -> list[tuple[str, int]]:

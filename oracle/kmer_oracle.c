@@ -100,6 +100,7 @@ typedef struct {
     const uint32_t* rank;
     uint32_t* counts;
     uint64_t total;
+    uint64_t* keys;      /* sparse mode (oracle_sparse_count): canonical codes appended here */
 } kstate;
 
 static inline void ks_reset(kstate* s) { s->len = 0; }
@@ -111,7 +112,8 @@ static inline void ks_push(kstate* s, uint8_t c) {
     s->rc = (s->rc >> 2) | ((uint64_t)(3 - code) << (2 * s->k - 2));
     if (++s->len >= (uint64_t)s->k) {
         uint64_t canon = s->fw < s->rc ? s->fw : s->rc;
-        s->counts[s->rank[canon]] += 1;
+        if (s->keys) s->keys[s->total] = canon;
+        else s->counts[s->rank[canon]] += 1;
         s->total += 1;
     }
 }
@@ -304,6 +306,38 @@ int oracle_count_many_parts(const uint8_t* bytes, const uint64_t* off, int n_gen
     }
     free(first);
     return rc;
+}
+
+static int cmp_u64(const void* a, const void* b) {
+    const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* get_kmers at any k = 1..31 (main.py:133-160: `jellyfish count -C` + `dump -c`
+ * keep the PRESENT canonical k-mers): the canonical standard code (A0 C1 G2 T3,
+ * the smaller of a k-mer and its reverse complement) of every window, sorted and
+ * run-length encoded: keys[i] ascending with counts[i], i < *n_out.  keys and
+ * counts hold at least len entries (keys is also the scratch of the sort). */
+int oracle_sparse_count(const uint8_t* bytes, uint64_t len, int k, int fmt, uint64_t* keys, uint32_t* counts,
+                        uint64_t* n_out) {
+    if (k < 1 || k > 31) return -1;
+    kstate s;
+    memset(&s, 0, sizeof s);
+    s.k = k;
+    s.mask = (1ull << (2 * k)) - 1;
+    s.keys = keys;
+    if (sniff(bytes, len, fmt) == 2) scan_fastq(&s, bytes, len);
+    else scan_fasta(&s, bytes, len);
+    qsort(keys, s.total, sizeof(uint64_t), cmp_u64);
+    uint64_t n = 0;
+    for (uint64_t i = 0; i < s.total; ++i) {
+        if (n && keys[n - 1] == keys[i]) { counts[n - 1] += 1; continue; }
+        keys[n] = keys[i];
+        counts[n] = 1;
+        ++n;
+    }
+    *n_out = n;
+    return 0;
 }
 
 int oracle_max_threads(void) {

@@ -1,0 +1,167 @@
+"""GPU parity of the sparse counter (kf_sparse_count: get_kmers at k = 2..31,
+reference kf2vec/main.py:112-176) against the oracle's sort-based restatement
+(oracle/kmer_oracle.c oracle_sparse_count) and against the dense counter where
+both exist (k <= 12).  Keys and counts must be bit-exact."""
+import numpy as np
+import pytest
+
+import gen
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev(native):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests need an MI355X")
+    return torch.device("cuda:0")
+
+
+_sparse = {}
+
+
+def sparse_counter(k, dev):
+    from kf2vecfsw_amd.counter import SparseCounter
+    if k not in _sparse:
+        _sparse[k] = SparseCounter(k, dev)
+    return _sparse[k]
+
+
+def run_sparse(blobs, k, dev, fmt=0):
+    import torch
+    from kf2vecfsw_amd import counter as C
+    hb = C.pack_genomes(blobs, fmt=fmt)
+    sc = sparse_counter(k, dev)
+    keys, cnts, nu = sc.count(C.to_device(hb, dev), int(hb.off[-1]))
+    torch.cuda.synchronize()
+    return sc.to_host(keys, cnts, nu, hb.off)
+
+
+def check(oracle, blobs, k, got, fmt=0, tag=""):
+    for i, b in enumerate(blobs):
+        ek, ec = oracle.sparse_count(b, k, fmt)
+        gk, gc = got[i]
+        assert gk.size == ek.size, (tag, i, k, gk.size, ek.size)
+        if not (np.array_equal(gk, ek) and np.array_equal(gc, ec)):
+            bad = np.nonzero((gk != ek) | (gc != ec))[0][:5]
+            pytest.fail(f"{tag} genome {i} k={k}: {bad.size}+ rows differ, first {bad.tolist()}: "
+                        f"got {gk[bad].tolist()}/{gc[bad].tolist()} want {ek[bad].tolist()}/{ec[bad].tolist()}")
+
+
+@pytest.mark.parametrize("k", [2, 3, 5, 8, 12, 13, 15, 16, 17, 21, 25, 31])
+def test_sparse_random_fasta_vs_oracle(torch_dev, oracle, k):
+    """Multi-record FASTA with N runs, IUPAC, lowercase, CRLF, blank lines,
+    1-column lines; plus an empty genome, a header-only one and one shorter than k."""
+    rng = np.random.default_rng(1000 + k)
+    blobs = [gen.random_fasta(rng, int(rng.integers(0, 30000)), n_rate=0.02, iupac_rate=0.002, lower=0.1,
+                              crlf_rate=0.2, poly_rate=0.5) for _ in range(6)]
+    blobs += [b"", b">only a header\n", b">s\nACG\n", b"ACGTTGCA" * 5]
+    check(oracle, blobs, k, run_sparse(blobs, k, torch_dev), tag="random")
+
+
+@pytest.mark.parametrize("k", [13, 31])
+def test_sparse_fastq(torch_dev, oracle, k):
+    rng = np.random.default_rng(77 + k)
+    blobs = [gen.random_fastq(rng, 150, n_rate=0.01, multiline=bool(i % 2)) for i in range(3)]
+    check(oracle, blobs, k, run_sparse(blobs, k, torch_dev, fmt=2), fmt=2, tag="fastq")
+
+
+@pytest.mark.parametrize("k", [3, 7, 9, 11, 12])
+def test_sparse_equals_dense_rows(torch_dev, k):
+    """k <= 12: the sparse counter's keys are exactly the dense counter's non-zero
+    bins (same lexicographic order), with the same counts."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    rng = np.random.default_rng(5 + k)
+    blobs = [gen.random_fasta(rng, int(rng.integers(1000, 200000)), n_rate=0.01, lower=0.05) for _ in range(5)]
+    got = run_sparse(blobs, k, torch_dev)
+    kc = C.KmerCounter(k, torch_dev)
+    dense, _ = kc.count(C.to_device(C.pack_genomes(blobs), torch_dev))
+    torch.cuda.synchronize()
+    dense = C.counts_to_numpy(dense)
+    _, col2rep = C.tables(k)
+    # col2rep is the kf code (A0 C1 T2 G3) of each column's canonical k-mer; map to standard codes
+    kf2std = np.array([0, 1, 3, 2], np.uint64)
+    rep = col2rep.astype(np.uint64)
+    std = np.zeros_like(rep)
+    rc = np.zeros_like(rep)
+    for i in range(k):
+        d = kf2std[((rep >> np.uint64(2 * i)) & np.uint64(3)).astype(np.intp)]
+        std |= d << np.uint64(2 * i)
+        rc |= (np.uint64(3) - d) << np.uint64(2 * (k - 1 - i))
+    std = np.minimum(std, rc)   # the class's lexicographically smaller member
+    for i in range(len(blobs)):
+        nz = np.nonzero(dense[i])[0]
+        assert np.array_equal(got[i][0], std[nz]), i
+        assert np.array_equal(got[i][1], dense[i][nz]), i
+
+
+def test_sparse_tile_boundaries_and_many_genomes(torch_dev, oracle):
+    """Genome lengths around the 2048-slot tile (2047..2049, 4096 +- 1) and 300
+    small genomes in one batch (many tiles, many segments per scan)."""
+    rng = np.random.default_rng(9)
+    blobs = []
+    for L in [1, 2046, 2047, 2048, 2049, 4095, 4096, 4097, 6143, 6145]:
+        s = gen.random_seq(rng, L).tobytes()
+        blobs.append(s[:L])
+    blobs += [gen.random_fasta(rng, int(rng.integers(0, 3000))) for _ in range(300)]
+    for k in (13, 31):
+        check(oracle, blobs, k, run_sparse(blobs, k, torch_dev), tag=f"tiles k={k}")
+
+
+def test_sparse_low_complexity_runs(torch_dev, oracle):
+    """One key for a whole genome (poly-A: a single run of ~1M), two-key genomes,
+    and dinucleotide repeats: a run crossing hundreds of tiles."""
+    blobs = [b">a\n" + b"A" * 1000000 + b"\n", b"ACACACACAC" * 50000, b"TTTTTTTTTTTTTTTTTTTTTTTTT\n" * 4000,
+             b">x\n" + b"ACGT" * 100000]
+    for k in (13, 16, 17, 31):
+        check(oracle, blobs, k, run_sparse(blobs, k, torch_dev), tag=f"lowcx k={k}")
+
+
+def test_sparse_newline_runs_and_breaks(torch_dev, oracle):
+    """Long runs of blank lines between bases (windows span them), and '\\r' / N
+    breaks right at a thread's 8-byte boundary."""
+    blobs = [b">a\n" + b"ACGTACGTACGTAC" + b"\n" * 100000 + b"GTACGTTGCAACGT\n",
+             b"ACGTACG\nTACGTACGTAC\r\nGTACGTACGTACG\n" * 500,
+             (b"ACGTACGN" * 3000), b"\n" * 5000]
+    for k in (13, 20):
+        check(oracle, blobs, k, run_sparse(blobs, k, torch_dev), tag=f"nl k={k}")
+
+
+def test_sparse_large_genomes_k31(torch_dev, oracle):
+    """Two 5 Mbp device-synthesised genomes (BASELINE configs[1] genome size) at
+    k = 31 and 21 against the oracle."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    db = C.synth_device_batch(2, 5_000_000, 4242, device=torch_dev)
+    off = C.synth_layout(2, 5_000_000)
+    host = db.data.cpu().numpy()
+    for k in (21, 31):
+        sc = sparse_counter(k, torch_dev)
+        keys, cnts, nu = sc.count(db, int(off[-1]))
+        torch.cuda.synchronize()
+        got = sc.to_host(keys, cnts, nu, off)
+        blobs = [host[int(off[i]): int(off[i + 1])].tobytes() for i in range(2)]
+        check(oracle, blobs, k, got, tag=f"synth k={k}")
+        # every window of a 5 Mbp N-free genome is counted
+        assert int(got[0][1].sum(dtype=np.uint64)) == 5_000_000 - k + 1
+
+
+@pytest.mark.parametrize("k", [13, 21, 31])
+def test_cli_get_kmers_large_k_vs_oracle(torch_dev, toy, oracle, tmp_path, k):
+    """`get_kmers -k 13..31` .npy == main.py:147-172 restated on the oracle's
+    present k-mers (rows in lexicographic order)."""
+    from kf2vecfsw_amd import main as M
+    inp, out = tmp_path / "in", tmp_path / "out"
+    inp.mkdir()
+    small = [t for t in toy if len(t[2]) < 1_000_000]   # the Python restatement is per character
+    for name, sample, data, exp in small:
+        (inp / name).write_bytes(data)
+    M.main(["get_kmers", "-input_dir", str(inp), "-output_dir", str(out), "-k", str(k)])
+    for name, sample, data, exp in small:
+        m = np.load(out / f"{sample}_k{k}.npy")
+        keys, cnts = oracle.sparse_count(data, k)
+        ref = oracle.kmers_matrix_from_dump(list(zip(oracle.std_code_text(keys, k), cnts.tolist())), k)
+        assert m.dtype == np.float32 and m.shape == (keys.size, k + 1), sample
+        assert np.array_equal(m, ref), sample

@@ -268,3 +268,32 @@ def test_write_kf_segments_generated_names(native, oracle, tmp_path):
     assert rc == 0, N.lib().kf_last_error()
     names = [pre[p] + "{}-{}".format(s + 1, s + CH.CHUNK_SZ) for p, s in zip(rpre.tolist(), rpos.tolist())]
     assert open(path).read() == "".join(oracle.kf_line(n, r, raw_cnt=True) for n, r in zip(names, rows))
+
+
+def test_sparse_kmers_matrix_matches_reference_restatement(native, oracle):
+    """get_kmers at k > 12: sparse_kmers_matrix (product) on the oracle's present
+    k-mers == main.py:147-172 restated on the same k-mers as `dump -c` lines."""
+    from kf2vecfsw_amd.main import sparse_kmers_matrix
+    data = gzip.open(os.path.join(TOY, "test_fna", "G000830275sub.fna.gz")).read()
+    for k in (13, 21, 31):
+        keys, cnts = oracle.sparse_count(data, k)
+        got = sparse_kmers_matrix(keys, cnts, k)
+        exp = oracle.kmers_matrix_from_dump(list(zip(oracle.std_code_text(keys, k), cnts.tolist())), k)
+        assert got.dtype == np.float32 and got.shape == exp.shape == (keys.size, k + 1)
+        assert np.array_equal(got, exp)
+    assert sparse_kmers_matrix(np.zeros(0, np.uint64), np.zeros(0, np.uint32), 21).shape == (0, 22)
+
+
+def test_sparse_count_rejects_bad_args(native):
+    """kf_sparse_count argument checks (no kernel is launched) and the workspace size."""
+    from kf2vecfsw_amd import _native as N
+    L = N.lib()
+    assert L.kf_sparse_count(None, None, 1, 100, None, 0, 32, None, 0, None, None, None, None) == N.KF_EINVAL
+    assert L.kf_sparse_count(None, None, 1, 100, None, 0, 1, None, 0, None, None, None, None) == N.KF_EINVAL
+    assert L.kf_sparse_count(None, None, 0, 0, None, 0, 21, None, 0, None, None, None, None) == N.KF_OK
+    assert L.kf_sparse_count(None, None, 1, 100, None, 0, 21, None, 0, None, None, None, None) == N.KF_EINVAL
+    assert b"null" in L.kf_last_error()
+    assert L.kf_sparse_count(None, None, 1, 1 << 32, None, 0, 21, None, 0, None, None, None, None) == N.KF_EINVAL
+    assert L.kf_sparse_workspace_bytes(32, 100, 1) == 0
+    w16, w17 = L.kf_sparse_workspace_bytes(16, 1 << 20, 4), L.kf_sparse_workspace_bytes(17, 1 << 20, 4)
+    assert (1 << 20) * 8 < w16 < w17   # u32 keys up to k = 16, u64 above; upos + histograms on top

@@ -164,3 +164,17 @@ def test_refpp_npy_oracle_and_product(oracle):
         assert exp.dtype == np.float32 and np.array_equal(ref, exp), e["file"]
         got = kmers_matrix(c, e["k"])
         assert got.dtype == np.float32 and np.array_equal(got, exp), e["file"]
+
+
+def test_sparse_oracle_equals_dense_oracle(oracle):
+    """oracle_sparse_count (sort + run-length, any k <= 31) against the pinned dense
+    restatement: the same present k-mers and counts for k = 2..9 on a toy genome."""
+    import gzip
+    data = gzip.open(os.path.join(TOY, "test_fna", "G000402355sub.fna.gz")).read()
+    for k in range(2, 10):
+        keys, cnts = oracle.sparse_count(data, k)
+        c, tot = oracle.count(data, k)
+        nz = np.nonzero(c)[0]
+        vocab = oracle.vocab_text(k).split()
+        assert [vocab[i].decode() for i in nz] == oracle.std_code_text(keys, k)
+        assert np.array_equal(c[nz], cnts) and int(cnts.sum()) == tot

@@ -1,0 +1,7 @@
+#!/bin/bash
+# round 4, call 10: first GPU run of the sparse counter (get_kmers k = 2..31)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/r04
+timeout -k 10 400 python -u -m pytest tests/test_gpu_sparse.py -m gpu -x -v --timeout 120 --timeout-method thread \
+    > gpurun_out/r04/v10_pytest_sparse.log 2>&1
