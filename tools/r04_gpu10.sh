@@ -1,7 +1,9 @@
 #!/bin/bash
-# round 4, call 10: first GPU run of the sparse counter (get_kmers k = 2..31)
+# round 4, call 10: first GPU run of the sparse counter (get_kmers k = 2..31) and its throughput
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/r04
 timeout -k 10 400 python -u -m pytest tests/test_gpu_sparse.py -m gpu -x -v --timeout 120 --timeout-method thread \
-    > gpurun_out/r04/v10_pytest_sparse.log 2>&1
+    > gpurun_out/r04/v10_pytest_sparse.log 2>&1 &&
+timeout -k 10 200 python -u tools/sparse_bench.py --genomes 64 --reps 5 \
+    > gpurun_out/r04/v10_sparse_bench.json 2> gpurun_out/r04/v10_sparse_bench.err
