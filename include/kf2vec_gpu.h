@@ -216,6 +216,15 @@ int kf_write_kf_segments(int32_t n_seg, const char* const* paths, const int32_t*
                          const uint32_t* counts, uint64_t nbins, int pseudocount,
                          int raw_cnt, int n_threads);
 
+/* kf_write_kf_segments for u16 counts (a get_chunks window of 10 kbp has every
+ * count below 2^16, so its rows cross PCIe at half the bytes). */
+int kf_write_kf_segments16(int32_t n_seg, const char* const* paths, const int32_t* seg_row0,
+                           const uint8_t* seg_append, const char* const* names,
+                           const char* const* prefixes, const uint32_t* row_prefix,
+                           const uint64_t* row_start, uint32_t win_len,
+                           const uint16_t* counts, uint64_t nbins, int pseudocount,
+                           int raw_cnt, int n_threads);
+
 /* ---- get_chunks device pre-pass (replaces seqtk seq -l 0 | awk N-collapse |
  * seqkit seq -g -m, main.py:726-760).  d_seq holds n_rec sorted, disjoint
  * [start, end) byte ranges of record sequences (the bytes between a header's

@@ -51,6 +51,8 @@ SIGNATURES = {
     "kf_write_kf_rows": (_int, [_cp, ctypes.POINTER(_cp), _i32, _vp, _u64, _int, _int, _int]),
     "kf_write_kf_segments": (_int, [_i32, ctypes.POINTER(_cp), _vp, _vp, ctypes.POINTER(_cp), ctypes.POINTER(_cp),
                                     _vp, _vp, _u32, _vp, _u64, _int, _int, _int]),
+    "kf_write_kf_segments16": (_int, [_i32, ctypes.POINTER(_cp), _vp, _vp, ctypes.POINTER(_cp), ctypes.POINTER(_cp),
+                                      _vp, _vp, _u32, _vp, _u64, _int, _int, _int]),
     "kf_chunk_compact": (_int, [_vp, _u64, _vp, _i32, _vp, _vp, _vp, _u64, _vp]),
     "kf_chunk_gather": (_int, [_vp, _vp, _i32, _u32, _vp, _vp]),
     "kf_sparse_workspace_bytes": (_u64, [_int, _u64, _i32]),

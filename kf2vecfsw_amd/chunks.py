@@ -19,8 +19,9 @@ Here the genomes are processed in batches of files:
 * the windows are gathered into a device buffer (``kf_chunk_gather``) and
   counted by ``kf_count_batch`` in launches of at most ``max_windows`` windows
   (the count matrix is 4 x bins bytes per window: 32 KiB at k=7, 8 MiB at k=11);
-* a writer thread formats and writes each launch's rows while the device counts
-  the next launch (``kf_write_kf_segments``: rows formatted by host threads,
+* the count rows come back as uint16 on a copy stream of their own, and a
+  writer thread formats and writes each launch's rows while the device counts
+  the next launch (``kf_write_kf_segments16``: rows formatted by host threads,
   one file per genome written in parallel, appended when a genome's windows span
   several launches).
 """
@@ -39,6 +40,7 @@ from . import _native as N
 
 CHUNK_SZ = 10000       # main.py:100
 CHUNK_CNT_THR = 5      # main.py:101
+assert CHUNK_SZ < 1 << 16   # window counts fit uint16 (count_and_write)
 LAUNCH_WINDOWS = 4096  # windows per count launch at most (128 MiB of k=7 counts)
 
 # KF_TRACE=1: stage timeline (host ms since the first event) for tools/chunks_bench.py
@@ -156,6 +158,9 @@ class ChunkPipeline:
         self.writer = ThreadPoolExecutor(max_workers=1)   # launches are written in order
         self.pending = []
         self._wbuf = None
+        # count rows go back on their own stream, so the next batch's H2D (on the
+        # compute stream) overlaps them (PCIe is full duplex)
+        self.d2h = torch.cuda.Stream(self.device)
 
     # ------------------------------------------------------------ pre-pass
     def prepare(self, hb, genomes: list[Genome]) -> torch.Tensor:
@@ -260,10 +265,19 @@ class ChunkPipeline:
             off = torch.arange(0, (nw + 1) * CHUNK_SZ, CHUNK_SZ, dtype=torch.int64, device=dev)
             db = DeviceBatch(self._wbuf, off, torch.zeros(2, dtype=torch.int64, device=dev), nw, 0)
             counts, _ = self.counter.count(db)
-            host = torch.empty(counts.shape, dtype=counts.dtype, pin_memory=True)
-            host.copy_(counts, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
+            # a window has at most CHUNK_SZ - k + 1 < 2^16 k-mers: its counts cross
+            # PCIe as uint16 bit patterns (half the bytes of the u32 rows)
+            c16 = counts.to(torch.int16)
+            del counts
+            done = torch.cuda.Event()
+            done.record(stream)
+            self.d2h.wait_event(done)
+            host = torch.empty(c16.shape, dtype=torch.int16, pin_memory=True)
+            with torch.cuda.stream(self.d2h):
+                host.copy_(c16, non_blocking=True)
+                c16.record_stream(self.d2h)
+                ev = torch.cuda.Event()
+                ev.record(self.d2h)
             # the segments of this launch: each genome's rows inside [w0, w1)
             segs = []
             for gi, g in enumerate(work):
@@ -277,7 +291,7 @@ class ChunkPipeline:
                 self.pending.pop(0).result()
             futs.append(self.writer.submit(self._write, ev, host, args))
             self.pending.append(futs[-1])
-            del counts
+            del c16
         return futs
 
     def _write_args(self, segs):
@@ -313,11 +327,11 @@ class ChunkPipeline:
             return
         t0 = time.perf_counter()
         n_seg, paths, row0, app, _enc, arr, rpre, rpos = args
-        rows = host.numpy().view(np.uint32)
-        N.check(N.lib().kf_write_kf_segments(n_seg, paths, row0.ctypes.data, app.ctypes.data, None, arr,
-                                             rpre.ctypes.data, rpos.ctypes.data, CHUNK_SZ, rows.ctypes.data,
-                                             rows.shape[1], int(self.pseudocount), 1, self.threads),
-                "kf_write_kf_segments")
+        rows = host.numpy().view(np.uint16)
+        N.check(N.lib().kf_write_kf_segments16(n_seg, paths, row0.ctypes.data, app.ctypes.data, None, arr,
+                                               rpre.ctypes.data, rpos.ctypes.data, CHUNK_SZ, rows.ctypes.data,
+                                               rows.shape[1], int(self.pseudocount), 1, self.threads),
+                "kf_write_kf_segments16")
         _tr("format_write", t0, segs=n_seg)
 
     def drain(self) -> None:

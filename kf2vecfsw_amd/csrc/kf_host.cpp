@@ -277,9 +277,21 @@ const SmallText& small_text() {
     return t;
 }
 
+// eight counts from c (u32 or u16) as two vectors of four u32
+inline void load8(const uint32_t* c, __m128i& a, __m128i& b) {
+    a = _mm_loadu_si128((const __m128i*)c);
+    b = _mm_loadu_si128((const __m128i*)(c + 4));
+}
+inline void load8(const uint16_t* c, __m128i& a, __m128i& b) {
+    const __m128i x = _mm_loadu_si128((const __m128i*)c);
+    a = _mm_unpacklo_epi16(x, _mm_setzero_si128());
+    b = _mm_unpackhi_epi16(x, _mm_setzero_si128());
+}
+
 // columns [0, n) of one raw row, each followed by ','; m as in SmallText.  Adds the
 // number of zero columns to *zeros.
-inline char* raw_columns(const uint32_t* c, uint64_t n, int m, char* p, uint64_t* zeros) {
+template <typename CT>
+inline char* raw_columns(const CT* c, uint64_t n, int m, char* p, uint64_t* zeros) {
     const SmallText& T = small_text();
     auto one = [&](uint32_t v) {
         if (v < kSmall) {
@@ -302,8 +314,8 @@ inline char* raw_columns(const uint32_t* c, uint64_t n, int m, char* p, uint64_t
         __m128i z = _mm_setzero_si128();   // 32-bit lane counters, folded every 2^30 groups
         const uint64_t end = std::min<uint64_t>(n & ~7ull, i + (8ull << 30));
         for (; i < end; i += 8) {
-            const __m128i a = _mm_loadu_si128((const __m128i*)(c + i));
-            const __m128i b = _mm_loadu_si128((const __m128i*)(c + i + 4));
+            __m128i a, b;
+            load8(c + i, a, b);
             z = _mm_sub_epi32(z, _mm_add_epi32(_mm_cmpeq_epi32(a, zero), _mm_cmpeq_epi32(b, zero)));
             const __m128i ok = _mm_and_si128(_mm_cmplt_epi32(_mm_xor_si128(a, sgn), lim),
                                              _mm_cmplt_epi32(_mm_xor_si128(b, sgn), lim));
@@ -333,7 +345,8 @@ inline char* raw_columns(const uint32_t* c, uint64_t n, int m, char* p, uint64_t
 uint64_t kf_line_cap(size_t name_len, uint64_t nbins) { return name_len + 2 + nbins * 26; }
 
 // main.py:327-357
-uint64_t format_line(const char* name, const uint32_t* c, uint64_t nb, int pseudo, int raw, char* out) {
+template <typename T>
+uint64_t format_line(const char* name, const T* c, uint64_t nb, int pseudo, int raw, char* out) {
     char* p = out;
     const size_t nl = strlen(name);
     memcpy(p, name, nl);
@@ -484,11 +497,12 @@ bool pwrite_all(int fd, const char* buf, uint64_t len, uint64_t off) {
 // is one block.  Row i's name is names[i], or, with names == NULL,
 // prefixes[row_prefix[i]] + "<s+1>-<s+win_len>", s = row_start[i] (the seqkit
 // sliding window name of main.py:905-915).
-extern "C" int kf_write_kf_segments(int32_t n_seg, const char* const* paths, const int32_t* seg_row0,
-                                    const uint8_t* seg_append, const char* const* names,
-                                    const char* const* prefixes, const uint32_t* row_prefix, const uint64_t* row_start,
-                                    uint32_t win_len, const uint32_t* counts, uint64_t nbins, int pseudocount,
-                                    int raw_cnt, int n_threads) {
+namespace {
+template <typename T>
+int write_segments(int32_t n_seg, const char* const* paths, const int32_t* seg_row0, const uint8_t* seg_append,
+                   const char* const* names, const char* const* prefixes, const uint32_t* row_prefix,
+                   const uint64_t* row_start, uint32_t win_len, const T* counts, uint64_t nbins, int pseudocount,
+                   int raw_cnt, int n_threads) {
     if (n_seg < 0 || (n_seg && (!paths || !seg_row0))) return kf_fail(KF_EINVAL, "null argument");
     if (n_seg == 0) return KF_OK;
     const int32_t n = seg_row0[n_seg];
@@ -646,6 +660,25 @@ extern "C" int kf_write_kf_segments(int32_t n_seg, const char* const* paths, con
     }
     if (err.load()) return kf_fail(errmsg.rfind("out of", 0) == 0 ? KF_ERANGE : KF_EINVAL, "%s", errmsg.c_str());
     return KF_OK;
+}
+}  // namespace
+
+extern "C" int kf_write_kf_segments(int32_t n_seg, const char* const* paths, const int32_t* seg_row0,
+                                    const uint8_t* seg_append, const char* const* names,
+                                    const char* const* prefixes, const uint32_t* row_prefix, const uint64_t* row_start,
+                                    uint32_t win_len, const uint32_t* counts, uint64_t nbins, int pseudocount,
+                                    int raw_cnt, int n_threads) {
+    return write_segments(n_seg, paths, seg_row0, seg_append, names, prefixes, row_prefix, row_start, win_len, counts,
+                          nbins, pseudocount, raw_cnt, n_threads);
+}
+
+extern "C" int kf_write_kf_segments16(int32_t n_seg, const char* const* paths, const int32_t* seg_row0,
+                                      const uint8_t* seg_append, const char* const* names,
+                                      const char* const* prefixes, const uint32_t* row_prefix,
+                                      const uint64_t* row_start, uint32_t win_len, const uint16_t* counts,
+                                      uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
+    return write_segments(n_seg, paths, seg_row0, seg_append, names, prefixes, row_prefix, row_start, win_len, counts,
+                          nbins, pseudocount, raw_cnt, n_threads);
 }
 
 extern "C" int kf_write_kf_rows(const char* path, const char* const* names, int32_t n, const uint32_t* counts,

@@ -297,3 +297,32 @@ def test_sparse_count_rejects_bad_args(native):
     assert L.kf_sparse_workspace_bytes(32, 100, 1) == 0
     w16, w17 = L.kf_sparse_workspace_bytes(16, 1 << 20, 4), L.kf_sparse_workspace_bytes(17, 1 << 20, 4)
     assert (1 << 20) * 8 < w16 < w17   # u32 keys up to k = 16, u64 above; upos + histograms on top
+
+
+@pytest.mark.parametrize("pseudo", [0, 1])
+def test_write_kf_segments16_equals_u32(native, oracle, tmp_path, pseudo):
+    """kf_write_kf_segments16 (u16 rows, get_chunks' copy-back width) writes the same
+    bytes as the u32 writer: counts 0..9 (SIMD text), up to 65,535, rows with no
+    zero column (integer text) and an all-zero row; pseudocount on and off."""
+    import ctypes
+    from kf2vecfsw_amd import _native as N
+    rng = np.random.default_rng(33)
+    nb = 2080   # not a multiple of 8: the scalar tail too
+    rows = rng.integers(0, 4, size=(60, nb)).astype(np.uint32)
+    rows[:, ::13] = rng.integers(0, 65536, size=rows[:, ::13].shape)
+    rows[5] = rng.integers(1, 9, size=nb)
+    rows[6] = 0
+    names = [f"w{i}" for i in range(60)]
+    enc = (ctypes.c_char_p * 60)(*[n.encode() for n in names])
+    r0 = np.asarray([0, 25, 60], np.int32)
+    out = {}
+    for tag, arr, fn in (("u32", rows, N.lib().kf_write_kf_segments),
+                         ("u16", np.ascontiguousarray(rows.astype(np.uint16)), N.lib().kf_write_kf_segments16)):
+        paths = [str(tmp_path / f"{tag}_{j}.kf") for j in range(2)]
+        rc = fn(2, (ctypes.c_char_p * 2)(*[p.encode() for p in paths]), r0.ctypes.data, None, enc, None, None, None,
+                0, arr.ctypes.data, nb, pseudo, 1, 3)
+        assert rc == 0, N.lib().kf_last_error()
+        out[tag] = [open(p).read() for p in paths]
+    assert out["u16"] == out["u32"]
+    assert out["u32"][0] == "".join(oracle.kf_line(names[i], rows[i], pseudocount=bool(pseudo), raw_cnt=True)
+                                    for i in range(25))
