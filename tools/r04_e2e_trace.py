@@ -37,8 +37,9 @@ def main():
         for g in range(args.genomes):
             open(os.path.join(inp, "B%04d.fna" % g), "wb").write(bench.bacterial_like(rng, 5_000_000)[0])
         res = {}
-        for parts in args.parts.split(","):
-            os.environ["KF_BATCH_PARTS"] = parts
+        for parts in args.parts.split(","):   # "P" or "P:A" (KF_READ_AHEAD = A)
+            os.environ["KF_BATCH_PARTS"] = parts.split(":")[0]
+            os.environ["KF_READ_AHEAD"] = parts.split(":")[1] if ":" in parts else "2"
             walls, trace = [], None
             for r in range(4):
                 out = os.path.join(work, f"o{parts}_{r}")
