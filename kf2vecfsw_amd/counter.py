@@ -124,16 +124,22 @@ def pack_genomes(blobs: Sequence[bytes | np.ndarray], names: Sequence[str] | Non
 
 
 def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: int = N.KF_FMT_AUTO,
-               pin: bool = True, threads: int = 8, pool=None, times: dict | None = None) -> HostBatch:
+               pin: bool = True, threads: int = 8, pool=None, times: dict | None = None,
+               buf: torch.Tensor | None = None) -> HostBatch:
     """Read files straight into one (pinned) buffer and index their records; files
     are read and indexed by a thread pool (readinto and the ctypes call release the
-    GIL): `pool` if given (shared across batches), else one of `threads` workers."""
+    GIL): `pool` if given (shared across batches), else one of `threads` workers.
+    `buf`: a caller-owned (pinned) buffer of at least the batch's bytes to read
+    into instead of a fresh allocation (the caller makes sure no copy still reads it)."""
     from concurrent.futures import ThreadPoolExecutor
     import time
     t0 = time.perf_counter()
     sizes = [os.path.getsize(p) for p in paths]
     off = _layout(sizes)
-    data = _alloc_host(int(off[-1]), pin)
+    if buf is not None and buf.numel() >= max(int(off[-1]), ALIGN):
+        data = buf[: max(int(off[-1]), ALIGN)]
+    else:
+        data = _alloc_host(int(off[-1]), pin)
     d = data.numpy()
     if times is not None:
         times["alloc_ms"] = round((time.perf_counter() - t0) * 1e3, 3)

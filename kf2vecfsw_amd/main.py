@@ -234,7 +234,9 @@ def get_frequencies(args) -> None:
         return
     counter = KmerCounter(args.k, device)
     paths = [os.path.join(args.input_dir, f) for f in files_names]
-    batches = _batches(paths, _pipeline_budget(paths, getattr(args, "batch_gb", None)))
+    # the first two batches are a quarter and a half of the others, so that the
+    # first H2D and count start sooner
+    batches = _batches(paths, _pipeline_budget(paths, getattr(args, "batch_gb", None)), ramp=True)
     # the reference processes files in order and later ones overwrite earlier
     # ones with the same sample name: keep the last occurrence only
     last = {s: i for i, s in enumerate(samples_names)}
@@ -253,10 +255,22 @@ def get_frequencies(args) -> None:
     def now_ms():
         return round((time.perf_counter() - t_origin) * 1e3, 3)
 
-    def pack(idx):
+    # pinned input slots, reused round robin (a fresh pinned block per batch costs
+    # ~1 ms of allocation on the reader's path): batch i reads into slot i mod
+    # n_slots once the H2D that last read that slot has completed
+    slot_bytes = max(sum((os.path.getsize(paths[i]) + 15) // 16 * 16 for i in b) for b in batches)
+    n_slots = min(len(batches), int(os.environ.get("KF_READ_AHEAD", "2")) + 2)
+    slots = [torch.empty(max(slot_bytes, 16), dtype=torch.uint8, pin_memory=True) for _ in range(n_slots)]
+    slot_ev: list = [None] * n_slots
+
+    def pack(bi, idx):
         t0 = now_ms()
         tm = {}
-        hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool, times=tm)
+        j = bi % n_slots
+        if slot_ev[j] is not None:
+            slot_ev[j].synchronize()
+        hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool, times=tm,
+                        buf=slots[j])
         if trace:
             tr.append(("read", idx[0], t0, now_ms(), tm))
         return hb
@@ -271,7 +285,7 @@ def get_frequencies(args) -> None:
     depth = int(os.environ.get("KF_READ_AHEAD", "2"))   # batches being read ahead
     reader = ThreadPoolExecutor(max_workers=depth)
     writer = ThreadPoolExecutor(max_workers=1)
-    reads = deque(reader.submit(pack, batches[i]) for i in range(min(depth, len(batches))))
+    reads = deque(reader.submit(pack, i, batches[i]) for i in range(min(depth, len(batches))))
     # While the first batches are read: the side stream's first event and launch
     # and the device block for a batch (the caching allocator keeps it for this
     # stream) would otherwise cost ~2 ms between the first read and its H2D
@@ -303,15 +317,16 @@ def get_frequencies(args) -> None:
         if trace:
             tr.append(("got", bi, t_wait, now_ms()))
         if bi + depth < len(batches):
-            reads.append(reader.submit(pack, batches[bi + depth]))
+            reads.append(reader.submit(pack, bi + depth, batches[bi + depth]))
         with torch.cuda.stream(stream):
             if trace:
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
                 e[0].record(stream)
                 evs.append((bi, now_ms(), e))
             db = to_device(hb, device)
-            # the pinned input is released here: PyTorch's caching host allocator
-            # keeps the block from reuse until the H2D copy queued above has run
+            h2d_done = torch.cuda.Event()
+            h2d_done.record(stream)
+            slot_ev[bi % n_slots] = h2d_done   # the slot is free again once this copy has run
             del hb
             if trace:
                 e[1].record(stream)
