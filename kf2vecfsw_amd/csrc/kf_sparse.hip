@@ -132,30 +132,65 @@ __global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, in
     if (t == 0) tfirst[n] = carry;
 }
 
-// ---- 1. emit: thread = 8 consecutive bytes; its k-1 bases of context come from
-// a walk back over the bytes before it (newlines skipped; a break, an excluded
-// range or the genome start ends the walk), then it rolls forward.
+// ---- 1. emit: one wave per tile, thread = kEB consecutive bytes; its k-1 bases
+// of context come from a walk back over the bytes before it (newlines skipped; a
+// break, an excluded range or the genome start ends the walk), then it rolls
+// forward.  32 bytes per thread amortise the walk (up to k-1 + newline bytes).
+constexpr int kEB = 32;
+constexpr int kEThreads = kSTile / kEB;   // 64: one wave per tile
+static_assert(kEThreads == 64, "emit: one wave per tile");
+
 template <typename KeyT>
-__global__ void __launch_bounds__(kSBlock) sp_emit_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
-                                                          const uint32_t* tfirst, int n, const uint64_t* excl,
-                                                          uint32_t n_excl, int k, KeyT* __restrict__ keys) {
+__device__ __forceinline__ void store_keys(KeyT* dst, const KeyT (&v)[kEB], uint32_t cnt) {
+    constexpr int per = 16 / sizeof(KeyT);   // keys per 16-byte store
+    if (cnt == (uint32_t)kEB && ((uintptr_t)dst & 15u) == 0) {
+#pragma unroll
+        for (int j = 0; j < kEB; j += per) {
+            if constexpr (per == 2) {
+                *(ulonglong2*)(dst + j) = make_ulonglong2(v[j], v[j + 1]);
+            } else {
+                *(uint4*)(dst + j) = make_uint4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+            }
+        }
+    } else {
+        for (uint32_t j = 0; j < cnt; ++j) dst[j] = v[j];
+    }
+}
+
+template <typename KeyT>
+__global__ void __launch_bounds__(kEThreads) sp_emit_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
+                                                            const uint32_t* tfirst, int n, const uint64_t* excl,
+                                                            uint32_t n_excl, int k, KeyT* __restrict__ keys) {
     TileSpan ts;
     if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
-    const uint32_t q0 = threadIdx.x * kSPer;
+    const uint32_t q0 = threadIdx.x * kEB;
     if (q0 >= ts.cnt) return;
-    const uint32_t p0 = ts.base + q0, p1 = ts.base + min(q0 + kSPer, ts.cnt);
+    const uint32_t p0 = ts.base + q0, cnt = min((uint32_t)kEB, ts.cnt - q0);
     const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
     const uint64_t kmask = (1ull << (2 * k)) - 1;
     const int hi = 2 * k - 2;
-    uint32_t code[kSPer];
+    uint32_t code[kEB];
     bool any = false;
-    for (int j = 0; j < kSPer; ++j) {
-        code[j] = p0 + j < p1 ? sp_code(bytes[p0 + j]) : 4u;
-        any |= code[j] < 4;
+    if (cnt == (uint32_t)kEB && ((uintptr_t)(bytes + p0) & 15u) == 0) {   // two 16-byte loads
+        const uint4 a = *(const uint4*)(bytes + p0), b = *(const uint4*)(bytes + p0 + 16);
+        const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int j = 0; j < kEB; ++j) {
+            code[j] = sp_code((uint8_t)(wv[j >> 2] >> (8 * (j & 3))));
+            any |= code[j] < 4;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kEB; ++j) {
+            code[j] = (uint32_t)j < cnt ? sp_code(bytes[p0 + j]) : 4u;
+            any |= code[j] < 4;
+        }
     }
+    KeyT out[kEB];
     if (!any) {   // no base here: no window ends in these bytes (and no walk back over a newline run)
-        for (int j = 0; j < kSPer; ++j)
-            if (p0 + j < p1) keys[p0 + j] = sent;
+#pragma unroll
+        for (int j = 0; j < kEB; ++j) out[j] = sent;
+        store_keys(keys + p0, out, cnt);
         return;
     }
     // first excluded range ending after p0
@@ -181,22 +216,22 @@ __global__ void __launch_bounds__(kSBlock) sp_emit_kernel(const uint8_t* __restr
         back |= (uint64_t)c << (2 * m);
         ++m;
     }
-    uint64_t fw = 0, rc = 0;
-    int len = 0;
-    for (int i = m - 1; i >= 0; --i) {
-        const uint32_t c = (uint32_t)(back >> (2 * i)) & 3u;
-        fw = ((fw << 2) | c) & kmask;
-        rc = (rc >> 2) | ((uint64_t)(3u - c) << hi);
-        ++len;
-    }
-    KeyT out[kSPer];
-    for (int j = 0; j < kSPer; ++j) {
+    uint64_t fw = back, rc = 0;   // fw: the m context bases, most recent lowest
+    int len = m;
+    for (int i = 0; i < m; ++i) rc |= (uint64_t)(3u - ((uint32_t)(back >> (2 * i)) & 3u)) << (hi - 2 * i);
+    // the next excluded range's bounds (the thread's bytes rarely meet one)
+    uint64_t xs = ix < n_excl ? excl[2 * ix] : ~0ull, xe = ix < n_excl ? excl[2 * ix + 1] : ~0ull;
+#pragma unroll
+    for (int j = 0; j < kEB; ++j) {
         const uint32_t p = p0 + j;
         KeyT key = sent;
-        if (p < p1) {
-            while (ix < n_excl && excl[2 * ix + 1] <= p) ++ix;
-            const bool ex = ix < n_excl && excl[2 * ix] <= p;
-            const uint32_t c = ex ? 5u : code[j];
+        if ((uint32_t)j < cnt) {
+            while (p >= xe) {
+                ++ix;
+                xs = ix < n_excl ? excl[2 * ix] : ~0ull;
+                xe = ix < n_excl ? excl[2 * ix + 1] : ~0ull;
+            }
+            const uint32_t c = p >= xs ? 5u : code[j];
             if (c == 5) {
                 len = 0;
             } else if (c < 4) {
@@ -207,8 +242,7 @@ __global__ void __launch_bounds__(kSBlock) sp_emit_kernel(const uint8_t* __restr
         }
         out[j] = key;
     }
-    for (int j = 0; j < kSPer; ++j)
-        if (p0 + j < p1) keys[p0 + j] = out[j];
+    store_keys(keys + p0, out, cnt);
 }
 
 // ---- 2a. per-tile digit histogram (one row per digit: hist[d * hstride + t])
@@ -223,12 +257,11 @@ __global__ void __launch_bounds__(kSBlock) sp_hist_kernel(const KeyT* __restrict
     for (int i = tid; i < kSWaves * 256; i += kSBlock) (&wc[0][0])[i] = 0;
     __syncthreads();
     const uint32_t dmask = (1u << bits) - 1u;
+    // order does not matter here: one LDS add per key into the wave's counters
+    // (the ballot matching of the scatter costs ~60 VALU per 64 keys)
     for (int it = 0; it < kSPer; ++it) {
         const uint32_t li = w * kSWaveSpan + it * 64 + lane;
-        const bool v = li < ts.cnt;
-        const uint32_t d = v ? (uint32_t)(keys[ts.base + li] >> shift) & dmask : 0u;
-        const uint64_t m = match_digit(d, bits, __ballot(v));
-        if (v && __popcll(m & ((1ull << lane) - 1)) == 0) wc[w][d] += (uint32_t)__popcll(m);
+        if (li < ts.cnt) atomicAdd(&wc[w][(uint32_t)(keys[ts.base + li] >> shift) & dmask], 1u);
     }
     __syncthreads();
     if (tid <= (int)dmask) hist[(uint64_t)tid * hstride + blockIdx.x] = wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
@@ -447,7 +480,7 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     // the last pass must write kw: start in kw for an even number of passes
     KeyT* src = (passes % 2 == 0) ? kw : ka;
     KeyT* dst = (passes % 2 == 0) ? ka : kw;
-    hipLaunchKernelGGL(sp_emit_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, d_bytes, d_goff, tfirst, n, d_excl,
+    hipLaunchKernelGGL(sp_emit_kernel<KeyT>, dim3(grid), dim3(kEThreads), 0, s, d_bytes, d_goff, tfirst, n, d_excl,
                        (uint32_t)n_excl, k, src);
     for (int p = 0; p < passes; ++p) {
         const int shift = p * bits;
