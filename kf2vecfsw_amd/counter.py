@@ -298,6 +298,11 @@ class SparseCounter:
         """Per genome (keys uint64[m], counts uint32[m]) on the host: each genome's
         slice is gathered on the device and the batch copied back once."""
         nu = nuniq.cpu().numpy()
+        if nu.size and (nu == -1).any():   # UINT64_MAX: the library refused the offsets
+            raise N.NativeError("kf_sparse_count: genome offsets must be non-decreasing and end at or below "
+                                "batch_bytes (nothing was counted)")
+        if nu.size and (nu == -2).any():   # UINT64_MAX - 1: the device's order check failed
+            raise N.NativeError("kf_sparse_count: the sorted keys failed the device's order check")
         if nu.size == 0 or int(nu.sum()) == 0:
             return [(np.zeros(0, np.uint64), np.zeros(0, np.uint32)) for _ in range(nu.size)]
         idx = torch.cat([torch.arange(int(off[g]), int(off[g]) + int(nu[g]), device=keys.device)

@@ -97,6 +97,20 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum) 
     return before + inc - v;
 }
 
+// Ranking inside a wave-instruction of the stable scatter:
+//   1 (default): LDS atomics, one returning add per key into the wave's digit
+//     counter -- an LDS unit serves the lanes of one instruction that hit the
+//     same address in lane order, so ranks follow the keys' order;
+//   0: ballot matching (one ballot per digit bit; ~46 VALU per 64 keys), which
+//     needs no such ordering.
+// The heads kernel checks every genome's final order (a key below its
+// predecessor flags the call: all counts come back UINT64_MAX - 1), so an
+// ordering the hardware did not keep cannot pass silently.
+#ifndef KF_SPARSE_RANK
+#define KF_SPARSE_RANK 1
+#endif
+
+#if KF_SPARSE_RANK == 0
 // Lanes of the wave (among `valid`) whose digit equals this lane's: one ballot
 // per digit bit.
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, int bits, uint64_t valid) {
@@ -108,15 +122,27 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, int bits, uint64_t v
     }
     return m;
 }
+#endif
 
-// ---- tiles: tfirst[g] = exclusive prefix of ceil(len_g / kSTile), tfirst[n] = total
-__global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, int n, uint32_t* tfirst) {
+// ---- tiles: tfirst[g] = exclusive prefix of ceil(len_g / kSTile), tfirst[n] = total.
+// A goff that decreases or ends past batch_bytes (the buffers' size) sets
+// tfirst[n+1] and leaves every tile count at 0: nothing is read or written, and
+// every genome's distinct-k-mer count comes back as UINT64_MAX.
+__global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, int n, uint64_t batch_bytes,
+                                                        uint32_t* tfirst) {
     __shared__ uint32_t sh[1024];
+    __shared__ int bad;
     const int t = threadIdx.x;
+    if (t == 0) bad = goff[n] > batch_bytes;
+    __syncthreads();
+    for (int g = t; g < n; g += 1024)
+        if (goff[g + 1] < goff[g]) bad = 1;
+    __syncthreads();
+    const bool ok = !bad;
     uint32_t carry = 0;
     for (int base = 0; base < n; base += 1024) {
         const int g = base + t;
-        const uint32_t v = g < n ? (uint32_t)((goff[g + 1] - goff[g] + kSTile - 1) / kSTile) : 0u;
+        const uint32_t v = g < n && ok ? (uint32_t)((goff[g + 1] - goff[g] + kSTile - 1) / kSTile) : 0u;
         sh[t] = v;
         __syncthreads();
         for (int d = 1; d < 1024; d <<= 1) {
@@ -129,7 +155,10 @@ __global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, in
         carry += sh[1023];
         __syncthreads();
     }
-    if (t == 0) tfirst[n] = carry;
+    if (t == 0) {
+        tfirst[n] = carry;
+        tfirst[n + 1] = ok ? 0u : 1u;
+    }
 }
 
 // ---- 1. emit: one wave per tile, thread = kEB consecutive bytes; its k-1 bases
@@ -315,12 +344,17 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
         const bool v = li < ts.cnt;
         const KeyT x = v ? in[ts.base + li] : (KeyT)0;
         const uint32_t d = (uint32_t)(x >> shift) & dmask;
+#if KF_SPARSE_RANK == 0
         const uint64_t m = match_digit(d, bits, __ballot(v));
         const uint32_t r = (uint32_t)__popcll(m & lt);
         const uint32_t prior = wc[w][d];
         if (v && r == 0) wc[w][d] = prior + (uint32_t)__popcll(m);
-        key[it] = x;
         rank[it] = prior + r;
+#else
+        (void)lt;
+        rank[it] = v ? atomicAdd(&wc[w][d], 1u) : 0u;
+#endif
+        key[it] = x;
     }
     __syncthreads();
     {
@@ -361,12 +395,18 @@ __device__ __forceinline__ bool is_head(const KeyT* keys, uint32_t p, uint32_t g
 
 template <typename KeyT>
 __global__ void __launch_bounds__(kSBlock) sp_heads_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
-                                                           const uint32_t* tfirst, int n, uint32_t* heads) {
+                                                           uint32_t* tfirst, int n, uint32_t* heads) {
     __shared__ uint32_t wsum[kSWaves];
     TileSpan ts;
     if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
     uint32_t c = 0;
-    for (uint32_t i = threadIdx.x; i < ts.cnt; i += kSBlock) c += is_head(keys, ts.base + i, ts.gs) ? 1u : 0u;
+    bool disorder = false;
+    for (uint32_t i = threadIdx.x; i < ts.cnt; i += kSBlock) {
+        const uint32_t p = ts.base + i;
+        c += is_head(keys, p, ts.gs) ? 1u : 0u;
+        disorder |= p > ts.gs && keys[p] < keys[p - 1];
+    }
+    if (__ballot(disorder) && (threadIdx.x & 63) == 0) atomicOr(&tfirst[n + 1], 2u);   // the sort's self-check
     for (int d = 32; d >= 1; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d, 64);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -426,9 +466,18 @@ __global__ void __launch_bounds__(kSBlock) sp_counts_kernel(const uint64_t* goff
 // ---- 3d. distinct k-mers per genome (SENT dropped)
 template <typename KeyT>
 __global__ void __launch_bounds__(256) sp_nuniq_kernel(const KeyT* keys, const uint64_t* goff, int n,
-                                                       const uint32_t* nfull, KeyT sent, uint64_t* nuniq) {
+                                                       const uint32_t* nfull, const uint32_t* tfirst, KeyT sent,
+                                                       uint64_t* nuniq) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
+    if (tfirst[n + 1] & 1u) {   // invalid goff (sp_tiles_kernel): nothing was counted
+        nuniq[g] = ~0ull;
+        return;
+    }
+    if (tfirst[n + 1] & 2u) {   // the final order check failed (sp_heads_kernel)
+        nuniq[g] = ~1ull;
+        return;
+    }
     uint32_t nf = nfull[g * 256];
     const uint64_t ge = goff[g + 1];
     if (nf > 0 && keys[ge - 1] == sent) --nf;
@@ -449,7 +498,7 @@ SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
     L.hstride = (uint32_t)(batch_bytes / kSTile + (uint64_t)n + 1);
     uint64_t o = 0;
     L.tfirst = o;
-    o = al256(o + 4ull * ((uint64_t)n + 1));
+    o = al256(o + 4ull * ((uint64_t)n + 2));   // + the invalid-goff flag
     L.keys = o;
     o = al256(o + ks * batch_bytes);
     L.hist = o;
@@ -476,7 +525,7 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     const int bits_total = 2 * k;
     const int passes = (bits_total + 7) / 8;
     const int bits = (bits_total + passes - 1) / passes;
-    hipLaunchKernelGGL(sp_tiles_kernel, dim3(1), dim3(1024), 0, s, d_goff, n, tfirst);
+    hipLaunchKernelGGL(sp_tiles_kernel, dim3(1), dim3(1024), 0, s, d_goff, n, batch_bytes, tfirst);
     // the last pass must write kw: start in kw for an even number of passes
     KeyT* src = (passes % 2 == 0) ? kw : ka;
     KeyT* dst = (passes % 2 == 0) ? ka : kw;
@@ -502,7 +551,7 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
                        upos);
     hipLaunchKernelGGL(sp_counts_kernel, dim3(grid), dim3(kSBlock), 0, s, d_goff, tfirst, n, gtot, upos, d_counts);
     const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
-    hipLaunchKernelGGL(sp_nuniq_kernel<KeyT>, dim3((n + 255) / 256), dim3(256), 0, s, kw, d_goff, n, gtot, sent,
+    hipLaunchKernelGGL(sp_nuniq_kernel<KeyT>, dim3((n + 255) / 256), dim3(256), 0, s, kw, d_goff, n, gtot, tfirst, sent,
                        d_nuniq);
     return KF_OK;
 }

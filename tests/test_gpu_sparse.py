@@ -165,3 +165,25 @@ def test_cli_get_kmers_large_k_vs_oracle(torch_dev, toy, oracle, tmp_path, k):
         ref = oracle.kmers_matrix_from_dump(list(zip(oracle.std_code_text(keys, k), cnts.tolist())), k)
         assert m.dtype == np.float32 and m.shape == (keys.size, k + 1), sample
         assert np.array_equal(m, ref), sample
+
+
+def test_sparse_rejects_bad_offsets(torch_dev):
+    """Offsets past batch_bytes or decreasing: nothing is written, every genome's
+    count comes back as UINT64_MAX and SparseCounter.to_host raises."""
+    import torch
+    from kf2vecfsw_amd import _native as N
+    from kf2vecfsw_amd import counter as C
+    hb = C.pack_genomes([b">a\nACGTACGTACGTACGT\n", b">b\nGGGGCCCCAAAATTTT\n"])
+    db = C.to_device(hb, torch_dev)
+    sc = sparse_counter(13, torch_dev)
+    keys, cnts, nu = sc.count(db, int(hb.off[-1]) - 16)      # offsets end past batch_bytes
+    torch.cuda.synchronize()
+    assert (nu.cpu().numpy() == -1).all()
+    with pytest.raises(N.NativeError):
+        sc.to_host(keys, cnts, nu, hb.off)
+    bad = db.off.clone()
+    bad[1] = bad[2] + 16                                       # decreasing
+    db2 = C.DeviceBatch(db.data, bad, db.excl, db.n, db.n_excl)
+    keys, cnts, nu = sc.count(db2, int(hb.off[-1]) + 64)
+    torch.cuda.synchronize()
+    assert (nu.cpu().numpy() == -1).all()
