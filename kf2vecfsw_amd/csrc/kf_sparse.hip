@@ -38,10 +38,20 @@ namespace kf {
 namespace {
 
 constexpr int kSBlock = 256;                   // threads per workgroup (4 waves)
-constexpr uint32_t kSTile = 2048;              // key slots per tile
-constexpr int kSPer = kSTile / kSBlock;        // 8 slots per thread
 constexpr int kSWaves = kSBlock / 64;
-constexpr uint32_t kSWaveSpan = kSTile / kSWaves;   // 512 slots per wave
+constexpr int kEB = 32;                        // emit: bytes per thread
+// Key slots per tile: 8192 u32 keys (32 keys per digit run on average; the
+// scatter stages 32 KiB) or 2048 u64 keys (the 8192-key u64 tile needs 156 VGPRs
+// and 64 KiB of staging: measured slower, profiles/r04/v22_sparse_bench*.json).
+template <typename KeyT>
+struct TileOf {
+    static constexpr uint32_t tile = sizeof(KeyT) == 4 ? 8192u : 2048u;
+    static constexpr int per = tile / kSBlock;             // slots per thread
+    static constexpr uint32_t wave_span = tile / kSWaves;  // slots per wave
+    static constexpr int emit_threads = tile / kEB;        // emit: kEB bytes per thread
+    static_assert(emit_threads % 64 == 0 && emit_threads <= 1024, "emit: whole waves per tile");
+};
+constexpr uint32_t tile_for_k(int k) { return k <= 16 ? TileOf<uint32_t>::tile : TileOf<uint64_t>::tile; }
 
 // Standard 2-bit code of a byte: A0 C1 G2 T3 (either case), 4 = '\n', 5 = other.
 __device__ __forceinline__ uint32_t sp_code(uint8_t c) {
@@ -71,13 +81,13 @@ struct TileSpan {
 };
 
 __device__ __forceinline__ bool tile_span(const uint64_t* goff, const uint32_t* tfirst, int n, uint32_t t,
-                                          TileSpan& ts) {
+                                          TileSpan& ts, uint32_t span) {
     if (t >= tfirst[n]) return false;
     ts.g = (uint32_t)tile_genome(tfirst, n, t);
     ts.gs = (uint32_t)goff[ts.g];
     ts.ge = (uint32_t)goff[ts.g + 1];
-    ts.base = ts.gs + (t - tfirst[ts.g]) * kSTile;
-    ts.cnt = min(kSTile, ts.ge - ts.base);
+    ts.base = ts.gs + (t - tfirst[ts.g]) * span;
+    ts.cnt = min(span, ts.ge - ts.base);
     return true;
 }
 
@@ -124,12 +134,12 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, int bits, uint64_t v
 }
 #endif
 
-// ---- tiles: tfirst[g] = exclusive prefix of ceil(len_g / kSTile), tfirst[n] = total.
+// ---- tiles: tfirst[g] = exclusive prefix of ceil(len_g / span), tfirst[n] = total.
 // A goff that decreases or ends past batch_bytes (the buffers' size) sets
 // tfirst[n+1] and leaves every tile count at 0: nothing is read or written, and
 // every genome's distinct-k-mer count comes back as UINT64_MAX.
 __global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, int n, uint64_t batch_bytes,
-                                                        uint32_t* tfirst) {
+                                                        uint32_t span, uint32_t* tfirst) {
     __shared__ uint32_t sh[1024];
     __shared__ int bad;
     const int t = threadIdx.x;
@@ -142,7 +152,7 @@ __global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, in
     uint32_t carry = 0;
     for (int base = 0; base < n; base += 1024) {
         const int g = base + t;
-        const uint32_t v = g < n && ok ? (uint32_t)((goff[g + 1] - goff[g] + kSTile - 1) / kSTile) : 0u;
+        const uint32_t v = g < n && ok ? (uint32_t)((goff[g + 1] - goff[g] + span - 1) / span) : 0u;
         sh[t] = v;
         __syncthreads();
         for (int d = 1; d < 1024; d <<= 1) {
@@ -161,13 +171,10 @@ __global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, in
     }
 }
 
-// ---- 1. emit: one wave per tile, thread = kEB consecutive bytes; its k-1 bases
+// ---- 1. emit: thread = kEB consecutive bytes of a tile; its k-1 bases
 // of context come from a walk back over the bytes before it (newlines skipped; a
 // break, an excluded range or the genome start ends the walk), then it rolls
 // forward.  32 bytes per thread amortise the walk (up to k-1 + newline bytes).
-constexpr int kEB = 32;
-constexpr int kEThreads = kSTile / kEB;   // 64: one wave per tile
-static_assert(kEThreads == 64, "emit: one wave per tile");
 
 template <typename KeyT>
 __device__ __forceinline__ void store_keys(KeyT* dst, const KeyT (&v)[kEB], uint32_t cnt) {
@@ -187,11 +194,12 @@ __device__ __forceinline__ void store_keys(KeyT* dst, const KeyT (&v)[kEB], uint
 }
 
 template <typename KeyT>
-__global__ void __launch_bounds__(kEThreads) sp_emit_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
+__global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
                                                             const uint32_t* tfirst, int n, const uint64_t* excl,
                                                             uint32_t n_excl, int k, KeyT* __restrict__ keys) {
+    using T = TileOf<KeyT>;
     TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
     const uint32_t q0 = threadIdx.x * kEB;
     if (q0 >= ts.cnt) return;
     const uint32_t p0 = ts.base + q0, cnt = min((uint32_t)kEB, ts.cnt - q0);
@@ -279,17 +287,18 @@ template <typename KeyT>
 __global__ void __launch_bounds__(kSBlock) sp_hist_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
                                                           const uint32_t* tfirst, int n, int shift, int bits,
                                                           uint32_t* hist, uint32_t hstride) {
+    using T = TileOf<KeyT>;
     __shared__ uint32_t wc[kSWaves][256];
     TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     for (int i = tid; i < kSWaves * 256; i += kSBlock) (&wc[0][0])[i] = 0;
     __syncthreads();
     const uint32_t dmask = (1u << bits) - 1u;
     // order does not matter here: one LDS add per key into the wave's counters
     // (the ballot matching of the scatter costs ~60 VALU per 64 keys)
-    for (int it = 0; it < kSPer; ++it) {
-        const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+    for (int it = 0; it < T::per; ++it) {
+        const uint32_t li = w * T::wave_span + it * 64 + lane;
         if (li < ts.cnt) atomicAdd(&wc[w][(uint32_t)(keys[ts.base + li] >> shift) & dmask], 1u);
     }
     __syncthreads();
@@ -325,22 +334,24 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
                                                              const uint64_t* goff, const uint32_t* tfirst, int n,
                                                              int shift, int bits, const uint32_t* hist,
                                                              uint32_t hstride, const uint32_t* gtot) {
+    using T = TileOf<KeyT>;
     __shared__ uint32_t wc[kSWaves][256];   // per wave: digit counts, then the wave's base inside the digit
     __shared__ uint32_t lbase[256];         // tile-local start of each digit
     __shared__ uint32_t gdst[256];          // global slot of the digit's first key in this tile, minus lbase
     __shared__ uint32_t wsum[kSWaves];
-    __shared__ KeyT stage[kSTile];
+    extern __shared__ __attribute__((aligned(16))) uint8_t sp_dyn[];
+    KeyT* stage = (KeyT*)sp_dyn;   // T::tile keys (dynamic LDS: 32 KiB)
     TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     for (int i = tid; i < kSWaves * 256; i += kSBlock) (&wc[0][0])[i] = 0;
     __syncthreads();
     const uint32_t dmask = (1u << bits) - 1u;
     const uint64_t lt = (1ull << lane) - 1;
-    KeyT key[kSPer];
-    uint32_t rank[kSPer];
-    for (int it = 0; it < kSPer; ++it) {
-        const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+    KeyT key[T::per];
+    uint32_t rank[T::per];
+    for (int it = 0; it < T::per; ++it) {
+        const uint32_t li = w * T::wave_span + it * 64 + lane;
         const bool v = li < ts.cnt;
         const KeyT x = v ? in[ts.base + li] : (KeyT)0;
         const uint32_t d = (uint32_t)(x >> shift) & dmask;
@@ -373,8 +384,8 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
         gdst[d] = live ? ts.gs + gb + hist[(uint64_t)d * hstride + blockIdx.x] - lb : 0u;
     }
     __syncthreads();
-    for (int it = 0; it < kSPer; ++it) {
-        const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+    for (int it = 0; it < T::per; ++it) {
+        const uint32_t li = w * T::wave_span + it * 64 + lane;
         if (li < ts.cnt) {
             const uint32_t d = (uint32_t)(key[it] >> shift) & dmask;
             stage[lbase[d] + wc[w][d] + rank[it]] = key[it];
@@ -396,9 +407,10 @@ __device__ __forceinline__ bool is_head(const KeyT* keys, uint32_t p, uint32_t g
 template <typename KeyT>
 __global__ void __launch_bounds__(kSBlock) sp_heads_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
                                                            uint32_t* tfirst, int n, uint32_t* heads) {
+    using T = TileOf<KeyT>;
     __shared__ uint32_t wsum[kSWaves];
     TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
     uint32_t c = 0;
     bool disorder = false;
     for (uint32_t i = threadIdx.x; i < ts.cnt; i += kSBlock) {
@@ -418,14 +430,15 @@ template <typename KeyT>
 __global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
                                                             const uint32_t* tfirst, int n, const uint32_t* heads,
                                                             uint64_t* __restrict__ ukeys, uint32_t* __restrict__ upos) {
+    using T = TileOf<KeyT>;
     __shared__ uint32_t wsum[kSWaves];
     TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt = (1ull << lane) - 1;
     uint32_t hm = 0, mine = 0;   // head flags of this lane's slots
-    for (int it = 0; it < kSPer; ++it) {
-        const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+    for (int it = 0; it < T::per; ++it) {
+        const uint32_t li = w * T::wave_span + it * 64 + lane;
         const bool h = li < ts.cnt && is_head(keys, ts.base + li, ts.gs);
         hm |= (h ? 1u : 0u) << it;
         mine += (uint32_t)__popcll(__ballot(h));
@@ -434,11 +447,11 @@ __global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restri
     __syncthreads();
     uint32_t u = heads[blockIdx.x];
     for (int x = 0; x < w; ++x) u += wsum[x];
-    for (int it = 0; it < kSPer; ++it) {
+    for (int it = 0; it < T::per; ++it) {
         const bool h = (hm >> it) & 1u;
         const uint64_t b = __ballot(h);
         if (h) {
-            const uint32_t li = w * kSWaveSpan + it * 64 + lane;
+            const uint32_t li = w * T::wave_span + it * 64 + lane;
             const uint32_t j = u + (uint32_t)__popcll(b & lt);
             ukeys[ts.gs + j] = (uint64_t)keys[ts.base + li];
             upos[ts.gs + j] = ts.base + li - ts.gs;
@@ -450,9 +463,9 @@ __global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restri
 // ---- 3c. counts = distance to the next head; tiles index unique slots here
 __global__ void __launch_bounds__(kSBlock) sp_counts_kernel(const uint64_t* goff, const uint32_t* tfirst, int n,
                                                             const uint32_t* nfull, const uint32_t* upos,
-                                                            uint32_t* __restrict__ counts) {
+                                                            uint32_t* __restrict__ counts, uint32_t span) {
     TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts)) return;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, span)) return;
     const uint32_t nf = nfull[ts.g * 256];
     const uint32_t len = ts.ge - ts.gs;
     for (uint32_t i = threadIdx.x; i < ts.cnt; i += kSBlock) {
@@ -495,7 +508,7 @@ uint64_t al256(uint64_t x) { return (x + 255) & ~255ull; }
 SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
     SpLayout L;
     const uint64_t ks = k <= 16 ? 4 : 8;
-    L.hstride = (uint32_t)(batch_bytes / kSTile + (uint64_t)n + 1);
+    L.hstride = (uint32_t)(batch_bytes / tile_for_k(k) + (uint64_t)n + 1);
     uint64_t o = 0;
     L.tfirst = o;
     o = al256(o + 4ull * ((uint64_t)n + 2));   // + the invalid-goff flag
@@ -512,9 +525,21 @@ SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
 }
 
 template <typename KeyT>
+int sp_prepare() {   // the scatter's staging tile is dynamic LDS (64 KiB for u64 keys)
+    static bool done = false;
+    if (done) return KF_OK;
+    if (hipFuncSetAttribute((const void*)&sp_scatter_kernel<KeyT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(TileOf<KeyT>::tile * sizeof(KeyT))) != hipSuccess)
+        return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    done = true;
+    return KF_OK;
+}
+
+template <typename KeyT>
 int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t batch_bytes, const uint64_t* d_excl,
            uint64_t n_excl, int k, uint8_t* work, const SpLayout& L, uint64_t* d_keys, uint32_t* d_counts,
            uint64_t* d_nuniq, hipStream_t s) {
+    if (const int rc = sp_prepare<KeyT>()) return rc;
     uint32_t* tfirst = (uint32_t*)(work + L.tfirst);
     KeyT* kw = (KeyT*)(work + L.keys);     // the sorted keys end here
     KeyT* ka = (KeyT*)d_keys;              // d_keys doubles as the other sort buffer
@@ -525,11 +550,11 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     const int bits_total = 2 * k;
     const int passes = (bits_total + 7) / 8;
     const int bits = (bits_total + passes - 1) / passes;
-    hipLaunchKernelGGL(sp_tiles_kernel, dim3(1), dim3(1024), 0, s, d_goff, n, batch_bytes, tfirst);
+    hipLaunchKernelGGL(sp_tiles_kernel, dim3(1), dim3(1024), 0, s, d_goff, n, batch_bytes, TileOf<KeyT>::tile, tfirst);
     // the last pass must write kw: start in kw for an even number of passes
     KeyT* src = (passes % 2 == 0) ? kw : ka;
     KeyT* dst = (passes % 2 == 0) ? ka : kw;
-    hipLaunchKernelGGL(sp_emit_kernel<KeyT>, dim3(grid), dim3(kEThreads), 0, s, d_bytes, d_goff, tfirst, n, d_excl,
+    hipLaunchKernelGGL(sp_emit_kernel<KeyT>, dim3(grid), dim3(TileOf<KeyT>::emit_threads), 0, s, d_bytes, d_goff, tfirst, n, d_excl,
                        (uint32_t)n_excl, k, src);
     for (int p = 0; p < passes; ++p) {
         const int shift = p * bits;
@@ -538,7 +563,9 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
                            hist, L.hstride);
         hipLaunchKernelGGL(sp_scan_kernel, dim3((uint32_t)n, 1u << b), dim3(kSBlock), 0, s, hist, L.hstride, tfirst,
                            gtot);
-        hipLaunchKernelGGL(sp_scatter_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, src, dst, d_goff, tfirst, n,
+        hipLaunchKernelGGL(sp_scatter_kernel<KeyT>, dim3(grid), dim3(kSBlock), TileOf<KeyT>::tile * sizeof(KeyT), s,
+                           src, dst,
+                           d_goff, tfirst, n,
                            shift, b, hist, L.hstride, gtot);
         KeyT* t = src;
         src = dst;
@@ -549,7 +576,8 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     hipLaunchKernelGGL(sp_scan_kernel, dim3((uint32_t)n, 1), dim3(kSBlock), 0, s, hist, L.hstride, tfirst, gtot);
     hipLaunchKernelGGL(sp_unique_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, kw, d_goff, tfirst, n, hist, d_keys,
                        upos);
-    hipLaunchKernelGGL(sp_counts_kernel, dim3(grid), dim3(kSBlock), 0, s, d_goff, tfirst, n, gtot, upos, d_counts);
+    hipLaunchKernelGGL(sp_counts_kernel, dim3(grid), dim3(kSBlock), 0, s, d_goff, tfirst, n, gtot, upos, d_counts,
+                       TileOf<KeyT>::tile);
     const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
     hipLaunchKernelGGL(sp_nuniq_kernel<KeyT>, dim3((n + 255) / 256), dim3(256), 0, s, kw, d_goff, n, gtot, tfirst, sent,
                        d_nuniq);
