@@ -34,6 +34,9 @@ over (genome, ~1 MiB part) pairs on every host CPU this process may use
 ~5 Mbp genome files in tmpfs (BASELINE configs[2] shape): the pipelined CLI
 wall time, and the same work run stage by stage (read + record index, H2D,
 count, D2H, format + write) to show where the time goes.
+`sparse` (rank 0, N=1) is get_kmers' sparse counter (k=31 by default: the
+present canonical k-mers per genome by a device radix sort) on 64 of the
+synthetic genomes, genome 0 checked against the oracle.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--k 7]
   (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
@@ -82,6 +85,8 @@ def parse_args(argv=None):
     ap.add_argument("--verify", type=int, default=4, help="genomes per rank checked bit-exactly against the oracle")
     ap.add_argument("--e2e-genomes", type=int, default=64, help="CLI end-to-end files (0 = off; N=1 only)")
     ap.add_argument("--e2e-len", type=int, default=5_000_000)
+    ap.add_argument("--sparse-k", type=int, default=31, help="get_kmers sparse counter line (0 = off; N=1 only)")
+    ap.add_argument("--sparse-genomes", type=int, default=64)
     return ap.parse_args(argv)
 
 
@@ -503,6 +508,60 @@ def e2e_bench(args, dev) -> dict:
         shutil.rmtree(work, ignore_errors=True)
 
 
+def sparse_bench(args, dev) -> dict:
+    """get_kmers' sparse counter (kf_sparse_count, k = 13..31: the present
+    canonical k-mers per genome by a device radix sort) on --sparse-genomes of
+    the synthetic genomes (ids 0..n-1, resident in HBM), median of 5 launches
+    after one warm launch.  Genome 0 is checked against the oracle's restatement
+    and every genome's total against seq_len - k + 1 (outside the timing).
+    `roofline.achieved` counts the algorithmic bytes (FASTA read + 12 B per
+    distinct k-mer written); the sort itself moves ~24 B per key per 8-bit pass."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    k, n, L = args.sparse_k, args.sparse_genomes, args.seq_len
+    db = C.synth_device_batch(n, L, SEED, width=80, device=dev)
+    off = C.synth_layout(n, L)
+    nbytes = int(off[-1])
+    sc = C.SparseCounter(k, dev)
+    ms = []
+    for r in range(6):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        keys, cnts, nu = sc.count(db, nbytes)
+        e1.record()
+        torch.cuda.synchronize()
+        if r:
+            ms.append(e0.elapsed_time(e1))
+        if r < 5:
+            del keys, cnts, nu
+    med = float(np.median(ms))
+    nuh = nu.cpu().numpy()
+    O = _oracle()
+    g0 = sc.to_host(keys[: int(off[1])], cnts[: int(off[1])], nu[:1], off[:2])[0]
+    ek, ec = O.sparse_count(O.synth_genome(0, SEED, L, 80), k)
+    ok = bool(np.array_equal(g0[0], ek) and np.array_equal(g0[1], ec))
+    tot = torch.zeros(n, dtype=torch.int64, device=dev)
+    c64 = cnts.to(torch.int64) & 0xFFFFFFFF
+    for g in range(n):
+        tot[g] = c64[int(off[g]): int(off[g]) + int(nuh[g])].sum()
+    ok &= bool((tot.cpu().numpy() == L - k + 1).all())
+    alg = nbytes + 12 * int(nuh.sum())
+    passes = (2 * k + 7) // 8
+    key_b = 4 if k <= 16 else 8
+    del keys, cnts, nu, db, sc, tot, c64
+    torch.cuda.empty_cache()
+    return {"config": f"get_kmers sparse counter, k={k}, {n} synthetic {L / 1e6:g} Mbp genomes resident in HBM "
+                      f"(the present canonical k-mers and counts per genome)",
+            "value": round(n * L / (med * 1e-3) / 1e9, 3), "unit": "Gbases/s", "ms": round(med, 4),
+            "ms_runs": [round(x, 4) for x in ms], "distinct_per_genome": int(nuh.mean()),
+            "roofline": {"bound": "hbm", "achieved": round(alg / (med * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBPS,
+                         "unit": "GB/s", "frac": round(alg / (med * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+                         "alg_bytes_per_launch": alg,
+                         "design_bytes_per_launch": int(n * L * (1 + key_b + passes * 3 * key_b + 6 * key_b)),
+                         "note": f"LSD radix sort of {2 * k}-bit keys in {passes} passes of 3 x {key_b} B per key"},
+            "parity": "ok" if ok else "MISMATCH"}
+
+
 def main() -> None:
     args = parse_args()
 
@@ -638,6 +697,10 @@ def main() -> None:
         torch.cuda.empty_cache()
         out["e2e"] = e2e_bench(args, dev)
         ok &= out["e2e"]["parity"] == "ok"
+        out["parity"] = "ok" if ok else "MISMATCH"
+    if rank == 0 and world == 1 and args.sparse_k:
+        out["sparse"] = sparse_bench(args, dev)
+        ok &= out["sparse"]["parity"] == "ok"
         out["parity"] = "ok" if ok else "MISMATCH"
     if rank == 0 and world == 1 and not args.no_cpu:
         ids = [a + i * st for a, st, c in W.plan for i in range(c)]
