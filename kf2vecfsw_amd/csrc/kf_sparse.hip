@@ -27,7 +27,7 @@
 // kf_index_records) break it too, and a window never spans two genomes.
 //
 // Layout: genome g owns key slots [goff[g], goff[g+1]) in every buffer (a genome
-// has at most as many windows as bytes), cut into 2048-slot tiles; tile t of
+// has at most as many windows as bytes), cut into tiles (TileOf); tile t of
 // the batch belongs to the genome g with tfirst[g] <= t < tfirst[g+1].
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -98,11 +98,11 @@ def test_sparse_equals_dense_rows(torch_dev, k):
 
 
 def test_sparse_tile_boundaries_and_many_genomes(torch_dev, oracle):
-    """Genome lengths around the 2048-slot tile (2047..2049, 4096 +- 1) and 300
-    small genomes in one batch (many tiles, many segments per scan)."""
+    """Genome lengths around the tiles (2,048 slots for u64 keys, 8,192 for u32)
+    and 300 small genomes in one batch (many tiles, many segments per scan)."""
     rng = np.random.default_rng(9)
     blobs = []
-    for L in [1, 2046, 2047, 2048, 2049, 4095, 4096, 4097, 6143, 6145]:
+    for L in [1, 2046, 2047, 2048, 2049, 4095, 4096, 4097, 6143, 6145, 8191, 8192, 8193, 16383, 16385]:
         s = gen.random_seq(rng, L).tobytes()
         blobs.append(s[:L])
     blobs += [gen.random_fasta(rng, int(rng.integers(0, 3000))) for _ in range(300)]
