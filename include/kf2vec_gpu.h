@@ -88,6 +88,20 @@ int kf_index_records(const uint8_t* bytes, uint64_t len, int fmt, uint64_t base,
                      uint64_t* out_iv, uint64_t cap_pairs, uint64_t* n_pairs,
                      int* fmt_detected);
 
+/* The FASTA record index of a batch resident in HBM (what kf_index_records finds
+ * per file, found on the device so the host only copies the files): the header
+ * lines -- a line starting with '>' at a genome start or after '\n', up to its
+ * '\n' or the genome end -- as sorted [start, end) pairs d_excl[2i], d_excl[2i+1]
+ * (absolute positions; adjacent header lines stay separate pairs, which the
+ * count kernels treat alike).  *d_n_pairs (device) receives the number of
+ * header lines; only the first cap_pairs are written, so a caller reads it back
+ * and runs again with a larger table if it was exceeded.  batch_bytes = goff[n];
+ * d_scratch >= ceil(batch_bytes / 4096) + 1 words.  FASTA only (FASTQ needs
+ * kf_index_records' per-file state).  Asynchronous on `stream`. */
+int kf_index_fasta(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
+                   uint64_t batch_bytes, uint64_t* d_excl, uint64_t cap_pairs,
+                   uint64_t* d_n_pairs, uint32_t* d_scratch, uint64_t scratch_words, void* stream);
+
 /* Count canonical k-mers of a batch of genomes already resident in HBM
  * (replaces `jellyfish count -C` + `jellyfish dump -c`, main.py:309-323).
  *   d_bytes    : batch bytes, 16-byte aligned; genome g is

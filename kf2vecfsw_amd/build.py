@@ -18,7 +18,7 @@ BUILD = os.path.join(HERE, "_build")
 ARCH = os.environ.get("KF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES_HIP = ["kf_count.hip", "kf_bucket.hip", "kf_chunks.hip", "kf_sparse.hip"]
+SOURCES_HIP = ["kf_count.hip", "kf_bucket.hip", "kf_chunks.hip", "kf_sparse.hip", "kf_index.hip"]
 SOURCES_CPP = ["kf_host.cpp"]
 DEPS = SOURCES_HIP + SOURCES_CPP + ["kf_internal.h", "kf_front.h", "../../include/kf2vec_gpu.h"]
 

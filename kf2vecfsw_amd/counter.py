@@ -75,7 +75,7 @@ class HostBatch:
     """Genomes packed back to back: genome g = data[off[g]:off[g+1]]."""
     data: torch.Tensor          # uint8, (pinned) host
     off: np.ndarray             # uint64 [n+1]
-    excl: np.ndarray            # uint64 [2*m] absolute [start, end) pairs
+    excl: np.ndarray | None     # uint64 [2*m] absolute [start, end) pairs; None: FASTA indexed on the device
     names: list[str]
 
     @property
@@ -86,7 +86,10 @@ class HostBatch:
         """Sequence characters (excludes header/quality lines and newlines)."""
         d = self.data.numpy()
         nl = int(np.count_nonzero(d[: int(self.off[-1])] == 10))
-        ex = int((self.excl[1::2] - self.excl[0::2]).sum()) if self.excl.size else 0
+        excl = self.excl if self.excl is not None else np.concatenate(
+            [index_records(d[int(self.off[i]): int(self.off[i + 1])], N.KF_FMT_FASTA, int(self.off[i]))[0]
+             for i in range(self.n)] or [np.zeros(0, np.uint64)])
+        ex = int((excl[1::2] - excl[0::2]).sum()) if excl.size else 0
         return int(self.off[-1] - self.off[0]) - nl - ex
 
 
@@ -125,12 +128,15 @@ def pack_genomes(blobs: Sequence[bytes | np.ndarray], names: Sequence[str] | Non
 
 def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: int = N.KF_FMT_AUTO,
                pin: bool = True, threads: int = 8, pool=None, times: dict | None = None,
-               buf: torch.Tensor | None = None) -> HostBatch:
+               buf: torch.Tensor | None = None, index: bool = True) -> HostBatch:
     """Read files straight into one (pinned) buffer and index their records; files
     are read and indexed by a thread pool (readinto and the ctypes call release the
     GIL): `pool` if given (shared across batches), else one of `threads` workers.
     `buf`: a caller-owned (pinned) buffer of at least the batch's bytes to read
-    into instead of a fresh allocation (the caller makes sure no copy still reads it)."""
+    into instead of a fresh allocation (the caller makes sure no copy still reads it).
+    index=False: a batch of FASTA files is not indexed here (excl None: to_device
+    finds the header lines on the device, kf_index_fasta); a batch with a FASTQ
+    file is indexed on the host all the same."""
     from concurrent.futures import ThreadPoolExecutor
     import time
     t0 = time.perf_counter()
@@ -155,6 +161,8 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
                     raise IOError(f"short read on {paths[i]}")
                 got += n
         d[lo + sz: int(off[i + 1])] = 10
+        if not index and fmt != N.KF_FMT_FASTQ and not (fmt == N.KF_FMT_AUTO and sz > 0 and d[lo] == ord("@")):
+            return None   # FASTA: the device indexes it
         return index_records(d[lo: lo + sz], fmt, lo)[0]
 
     if pool is not None:
@@ -164,6 +172,10 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
             excl = list(ex.map(one, range(len(paths))))
     else:
         excl = [one(i) for i in range(len(paths))]
+    if not index and all(e is None for e in excl):
+        return HostBatch(data, off, None, list(names) if names else list(paths))
+    excl = [e if e is not None else index_records(d[int(off[i]): int(off[i]) + sizes[i]], N.KF_FMT_FASTA,
+                                                  int(off[i]))[0] for i, e in enumerate(excl)]
     ex = np.concatenate(excl) if excl else np.zeros(0, np.uint64)
     return HostBatch(data, off, ex.astype(np.uint64), list(names) if names else list(paths))
 
@@ -177,12 +189,42 @@ class DeviceBatch:
     n_excl: int
 
 
+def index_on_device(data: torch.Tensor, off: torch.Tensor, n: int, nbytes: int) -> tuple[torch.Tensor, int]:
+    """FASTA header lines of a device batch (kf_index_fasta) on the current
+    stream: (pairs int64[2m] on the device, m).  Reads m back (one small
+    synchronising copy); a table that was too small is grown and the index run
+    again, so the result is always complete."""
+    dev = data.device
+    s = _stream_ptr(dev)
+    nb = (nbytes + 4095) // 4096
+    scratch = torch.empty(nb + 1, dtype=torch.int32, device=dev)
+    npairs = torch.zeros(1, dtype=torch.int64, device=dev)
+    cap = nbytes // 64 + 16 * n + 1024   # a header every 64 bytes; more is re-run
+    while True:
+        excl = torch.empty(max(2 * cap, 2), dtype=torch.int64, device=dev)
+        N.check(N.lib().kf_index_fasta(data.data_ptr(), off.data_ptr(), n, nbytes, excl.data_ptr(), cap,
+                                       npairs.data_ptr(), scratch.data_ptr(), nb + 1, s), "kf_index_fasta")
+        m = int(npairs.item())
+        if m <= cap:
+            return excl[: 2 * m], m
+        cap = m
+
+
 def to_device(hb: HostBatch, device: torch.device | str = "cuda") -> DeviceBatch:
     """Asynchronous H2D of a batch on the current stream.  The small offset and
     interval tables are staged through pinned memory too: a copy from pageable
-    memory would block the host until the stream's earlier copies finish."""
+    memory would block the host until the stream's earlier copies finish.  A
+    batch packed without its record index (excl None) is indexed on the device
+    (index_on_device: one small synchronising copy)."""
     dev = torch.device(device)
     data = hb.data.to(dev, non_blocking=True)
+    if hb.excl is None:
+        pin = hb.data.is_pinned()
+        off = torch.from_numpy(hb.off.view(np.int64))
+        off = (off.pin_memory() if pin else off).to(dev, non_blocking=pin)
+        with torch.cuda.device(dev):
+            excl, m = index_on_device(data, off, hb.n, int(hb.off[-1]))
+        return DeviceBatch(data, off, excl if m else torch.zeros(2, dtype=torch.int64, device=dev), hb.n, m)
     ex = hb.excl if hb.excl.size else np.zeros(2, np.uint64)
     pin = hb.data.is_pinned()
     n_off = (hb.off.size + 1) & ~1   # the interval table starts 16-byte aligned

@@ -269,8 +269,10 @@ def get_frequencies(args) -> None:
         j = bi % n_slots
         if slot_ev[j] is not None:
             slot_ev[j].synchronize()
+        # FASTA batches are indexed on the device (to_device -> kf_index_fasta):
+        # the readers only copy the files
         hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool, times=tm,
-                        buf=slots[j])
+                        buf=slots[j], index=False)
         if trace:
             tr.append(("read", idx[0], t0, now_ms(), tm))
         return hb
