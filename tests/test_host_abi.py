@@ -326,3 +326,22 @@ def test_write_kf_segments16_equals_u32(native, oracle, tmp_path, pseudo):
     assert out["u16"] == out["u32"]
     assert out["u32"][0] == "".join(oracle.kf_line(names[i], rows[i], pseudocount=bool(pseudo), raw_cnt=True)
                                     for i in range(25))
+
+
+def test_pack_files_without_index(native, tmp_path):
+    """pack_files(index=False): a FASTA batch comes back unindexed (excl None: the
+    device indexes it); a batch holding a FASTQ file is indexed on the host, FASTA
+    files included, exactly as with index=True."""
+    from kf2vecfsw_amd import counter as C
+    fa = tmp_path / "a.fna"
+    fa.write_bytes(b">a\nACGT\n>b\nGG\n")
+    fb = tmp_path / "b.fa"
+    fb.write_bytes(b"ACGT\n>c x\nTT")
+    fq = tmp_path / "c.fq"
+    fq.write_bytes(b"@r1\nACGT\n+\nIIII\n")
+    hb = C.pack_files([str(fa), str(fb)], pin=False, threads=1, index=False)
+    assert hb.excl is None and hb.n == 2
+    assert hb.seq_chars() == C.pack_files([str(fa), str(fb)], pin=False, threads=1).seq_chars()
+    mixed = C.pack_files([str(fa), str(fq), str(fb)], pin=False, threads=1, index=False)
+    ref = C.pack_files([str(fa), str(fq), str(fb)], pin=False, threads=1)
+    assert mixed.excl is not None and np.array_equal(mixed.excl, ref.excl)
