@@ -38,7 +38,8 @@ namespace kf {
 // 2 (hashed stand-ins), 3 = no phase-1 rank atomics (dense path; the round counts
 // stay 0, so no records are written or read at all), 4 = no
 // phase-1 staging writes (dense path), 5 = no phase-2 histogram adds, 7 = rank
-// adds without returns, 8 = no phase 2 (rows stay zero).
+// adds without returns, 8 = no phase 2 (rows stay zero), 9 = as 1 with
+// lane-consecutive flush slots (no LDS bank conflicts in the flush).
 #ifndef KF_BK_ABL
 #define KF_BK_ABL 0
 #endif
@@ -816,6 +817,10 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             if (KF_BK_ABL == 1) {
                 const uint32_t x = (2 * g4) & (L::codes - 4u);
                 return v2u{x | (x + 1) << 16, (x + 2) | (x + 3) << 16};
+            }
+            if (KF_BK_ABL == 9) {   // no col_idx reads and lane-consecutive slots (no bank conflicts)
+                const uint32_t m = L::codes - 1u, x = (g4 >> 2) & m;
+                return v2u{x | ((x + 1024u) & m) << 16, ((x + 2048u) & m) | ((x + 3072u) & m) << 16};
             }
             return *(const v2u*)(B.col_idx + g4);
         };
