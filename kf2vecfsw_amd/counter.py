@@ -77,6 +77,8 @@ class HostBatch:
     off: np.ndarray             # uint64 [n+1]
     excl: np.ndarray | None     # uint64 [2*m] absolute [start, end) pairs; None: FASTA indexed on the device
     names: list[str]
+    dev_data: torch.Tensor | None = None   # the bytes already copied to the device (maybe on another stream)
+    dev_event: object = None               # ... and the event that copy recorded
 
     @property
     def n(self) -> int:
@@ -217,7 +219,14 @@ def to_device(hb: HostBatch, device: torch.device | str = "cuda") -> DeviceBatch
     batch packed without its record index (excl None) is indexed on the device
     (index_on_device: one small synchronising copy)."""
     dev = torch.device(device)
-    data = hb.data.to(dev, non_blocking=True)
+    if hb.dev_data is not None:   # copied already (get_frequencies' readers, on a copy stream)
+        cur = torch.cuda.current_stream(dev)
+        if hb.dev_event is not None:
+            cur.wait_event(hb.dev_event)
+        data = hb.dev_data
+        data.record_stream(cur)
+    else:
+        data = hb.data.to(dev, non_blocking=True)
     if hb.excl is None:
         pin = hb.data.is_pinned()
         off = torch.from_numpy(hb.off.view(np.int64))

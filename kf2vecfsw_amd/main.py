@@ -273,17 +273,26 @@ def get_frequencies(args) -> None:
         # the readers only copy the files
         hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool, times=tm,
                         buf=slots[j], index=False)
+        # the batch goes to the device on the copy stream as soon as it is read,
+        # so its H2D overlaps the previous batch's index, count and copy-back
+        with torch.cuda.stream(copy_stream):
+            hb.dev_data = hb.data.to(device, non_blocking=True)
+            hb.dev_event = torch.cuda.Event()
+            hb.dev_event.record(copy_stream)
+        slot_ev[j] = hb.dev_event   # the slot is free again once this copy has run
         if trace:
             tr.append(("read", idx[0], t0, now_ms(), tm))
         return hb
 
     # Three-stage pipeline over batches:
-    #   readers (2)   : read + record-index batches i+1, i+2 into pinned memory
-    #                   (one shared pool of -p file workers keeps all cores busy)
-    #   this thread   : H2D + count + D2H of batch i on a side stream (async)
+    #   readers (2)   : read batches i+1, i+2 into pinned memory (one shared pool
+    #                   of -p file workers keeps all cores busy) and put each on
+    #                   the copy stream as soon as it is read
+    #   this thread   : record index + count + D2H of batch i on a side stream
     #   writer thread : wait for batch i's copy-back, format + write its .kf files
     # The prints stay in the reference's per-file order (main.py:332-341).
     stream = torch.cuda.Stream(device)
+    copy_stream = torch.cuda.Stream(device)
     depth = int(os.environ.get("KF_READ_AHEAD", "2"))   # batches being read ahead
     reader = ThreadPoolExecutor(max_workers=depth)
     writer = ThreadPoolExecutor(max_workers=1)
@@ -293,11 +302,13 @@ def get_frequencies(args) -> None:
     # stream) would otherwise cost ~2 ms between the first read and its H2D
     # (KF_TRACE: got 0 -> issue 0, tools/e2e_bench.py).
     big = max(sum((os.path.getsize(paths[i]) + 15) // 16 * 16 for i in b) for b in batches)
-    with torch.cuda.stream(stream):
+    with torch.cuda.stream(copy_stream):   # the batches' device blocks come from the copy stream's pool
         warm = torch.empty(big + 16, dtype=torch.uint8, device=device)
         warm[:16].zero_()
-        torch.cuda.Event(enable_timing=True).record(stream)
         del warm
+    with torch.cuda.stream(stream):
+        torch.cuda.Event(enable_timing=True).record(stream)
+    copy_stream.synchronize()
     stream.synchronize()
     writes = []
     # batches whose .kf files may still be waiting for the writer: each holds a
@@ -326,9 +337,6 @@ def get_frequencies(args) -> None:
                 e[0].record(stream)
                 evs.append((bi, now_ms(), e))
             db = to_device(hb, device)
-            h2d_done = torch.cuda.Event()
-            h2d_done.record(stream)
-            slot_ev[bi % n_slots] = h2d_done   # the slot is free again once this copy has run
             del hb
             if trace:
                 e[1].record(stream)
