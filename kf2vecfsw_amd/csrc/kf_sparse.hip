@@ -41,11 +41,14 @@ constexpr int kSBlock = 256;                   // threads per workgroup (4 waves
 constexpr int kSWaves = kSBlock / 64;
 constexpr int kEB = 32;                        // emit: bytes per thread
 // Key slots per tile: 8192 u32 keys (32 keys per digit run on average; the
-// scatter stages 32 KiB) or 2048 u64 keys (the 8192-key u64 tile needs 156 VGPRs
-// and 64 KiB of staging: measured slower, profiles/r04/v22_sparse_bench*.json).
+// scatter stages 32 KiB) or 4096 u64 keys (16 per digit run: 128-byte runs; 2048
+// measured 3-9 % slower and 8192 4-18 % slower, profiles/r04/v28_*.json).
 template <typename KeyT>
 struct TileOf {
-    static constexpr uint32_t tile = sizeof(KeyT) == 4 ? 8192u : 2048u;
+#ifndef KF_SPARSE_TILE64   // u64 tile (tools/ A/B builds)
+#define KF_SPARSE_TILE64 4096
+#endif
+    static constexpr uint32_t tile = sizeof(KeyT) == 4 ? 8192u : (uint32_t)KF_SPARSE_TILE64;
     static constexpr int per = tile / kSBlock;             // slots per thread
     static constexpr uint32_t wave_span = tile / kSWaves;  // slots per wave
     static constexpr int emit_threads = tile / kEB;        // emit: kEB bytes per thread
@@ -176,34 +179,28 @@ __global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, in
 // break, an excluded range or the genome start ends the walk), then it rolls
 // forward.  32 bytes per thread amortise the walk (up to k-1 + newline bytes).
 
+// The keys go out through LDS: a thread's kEB keys are one row (padded by 16 bytes
+// against bank conflicts), read back key by key in lane order so that every store
+// instruction writes 256-512 contiguous bytes (a thread storing its own 128-256
+// bytes touches 64 lines per instruction).
+#ifndef KF_SPARSE_EMIT   // 1: whole rows staged, 2: half rows (half the LDS), 0: direct stores
+#define KF_SPARSE_EMIT 2
+#endif
 template <typename KeyT>
-__device__ __forceinline__ void store_keys(KeyT* dst, const KeyT (&v)[kEB], uint32_t cnt) {
-    constexpr int per = 16 / sizeof(KeyT);   // keys per 16-byte store
-    if (cnt == (uint32_t)kEB && ((uintptr_t)dst & 15u) == 0) {
-#pragma unroll
-        for (int j = 0; j < kEB; j += per) {
-            if constexpr (per == 2) {
-                *(ulonglong2*)(dst + j) = make_ulonglong2(v[j], v[j + 1]);
-            } else {
-                *(uint4*)(dst + j) = make_uint4(v[j], v[j + 1], v[j + 2], v[j + 3]);
-            }
-        }
-    } else {
-        for (uint32_t j = 0; j < cnt; ++j) dst[j] = v[j];
-    }
-}
+struct EmitStage {
+    static constexpr int keys = KF_SPARSE_EMIT == 2 ? kEB / 2 : kEB;   // keys per row per round
+    static constexpr int row = keys + 16 / (int)sizeof(KeyT);          // padded row
+    static constexpr int elems = KF_SPARSE_EMIT == 0 ? 1 : TileOf<KeyT>::emit_threads * row;
+};
 
+// One thread's keys (out[] holds SENT on entry): the windows ending in the kEB
+// bytes at p0 = ts.base + threadIdx.x * kEB.
 template <typename KeyT>
-__global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
-                                                            const uint32_t* tfirst, int n, const uint64_t* excl,
-                                                            uint32_t n_excl, int k, KeyT* __restrict__ keys) {
-    using T = TileOf<KeyT>;
-    TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
+__device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, const TileSpan& ts, uint32_t n_excl,
+                                         const uint64_t* excl, int k, KeyT (&out)[kEB]) {
     const uint32_t q0 = threadIdx.x * kEB;
     if (q0 >= ts.cnt) return;
     const uint32_t p0 = ts.base + q0, cnt = min((uint32_t)kEB, ts.cnt - q0);
-    const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
     const uint64_t kmask = (1ull << (2 * k)) - 1;
     const int hi = 2 * k - 2;
     uint32_t code[kEB];
@@ -223,13 +220,7 @@ __global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(con
             any |= code[j] < 4;
         }
     }
-    KeyT out[kEB];
-    if (!any) {   // no base here: no window ends in these bytes (and no walk back over a newline run)
-#pragma unroll
-        for (int j = 0; j < kEB; ++j) out[j] = sent;
-        store_keys(keys + p0, out, cnt);
-        return;
-    }
+    if (!any) return;   // no base here: no window ends in these bytes (and no walk back over a newline run)
     // first excluded range ending after p0
     uint32_t ix = 0;
     {
@@ -246,7 +237,24 @@ __global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(con
     const uint64_t floor_ = max((uint64_t)ts.gs, stop);
     uint64_t back = 0;
     int m = 0;
-    for (uint64_t q = p0; q > floor_ && m < k - 1;) {
+    uint64_t q = p0;
+    bool open = true;   // the walk may go on
+    if (p0 >= floor_ + kEB && (p0 & 15u) == 0) {
+        // the kEB bytes before p0 in two 16-byte loads (no chain of dependent
+        // byte loads), walked in registers
+        const uint4 a = *(const uint4*)(bytes + p0 - kEB), b = *(const uint4*)(bytes + p0 - 16);
+        const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int j = kEB - 1; j >= 0; --j) {
+            const uint32_t c = sp_code((uint8_t)(wv[j >> 2] >> (8 * (j & 3))));
+            if (open && m < k - 1 && c != 4) {
+                if (c == 5) open = false;
+                else back |= (uint64_t)c << (2 * m++);
+            }
+        }
+        q = p0 - kEB;
+    }
+    for (; open && q > floor_ && m < k - 1;) {
         const uint32_t c = sp_code(bytes[--q]);
         if (c == 4) continue;
         if (c == 5) break;
@@ -261,7 +269,6 @@ __global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(con
 #pragma unroll
     for (int j = 0; j < kEB; ++j) {
         const uint32_t p = p0 + j;
-        KeyT key = sent;
         if ((uint32_t)j < cnt) {
             while (p >= xe) {
                 ++ix;
@@ -274,12 +281,63 @@ __global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(con
             } else if (c < 4) {
                 fw = ((fw << 2) | c) & kmask;
                 rc = (rc >> 2) | ((uint64_t)(3u - c) << hi);
-                if (++len >= k) key = (KeyT)(fw < rc ? fw : rc);
+                if (++len >= k) out[j] = (KeyT)(fw < rc ? fw : rc);
             }
         }
-        out[j] = key;
     }
-    store_keys(keys + p0, out, cnt);
+}
+
+template <typename KeyT>
+__global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
+                                                            const uint32_t* tfirst, int n, const uint64_t* excl,
+                                                            uint32_t n_excl, int k, KeyT* __restrict__ keys) {
+    using T = TileOf<KeyT>;
+    using S = EmitStage<KeyT>;
+    __shared__ __attribute__((aligned(16))) KeyT stage[S::elems];
+    TileSpan ts;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;   // uniform over the workgroup
+    const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
+    KeyT out[kEB];
+#pragma unroll
+    for (int j = 0; j < kEB; ++j) out[j] = sent;
+    emit_row(bytes, ts, n_excl, excl, k, out);
+#if KF_SPARSE_EMIT == 0
+    (void)stage;
+    const uint32_t q0 = threadIdx.x * kEB;
+    if (q0 < ts.cnt) {
+        KeyT* dst = keys + ts.base + q0;
+        const uint32_t cnt = min((uint32_t)kEB, ts.cnt - q0);
+        if (cnt == (uint32_t)kEB && ((uintptr_t)dst & 15u) == 0) {
+#pragma unroll
+            for (int j = 0; j < kEB; j += 16 / (int)sizeof(KeyT)) {
+                if constexpr (sizeof(KeyT) == 8) *(ulonglong2*)(dst + j) = make_ulonglong2(out[j], out[j + 1]);
+                else *(uint4*)(dst + j) = make_uint4(out[j], out[j + 1], out[j + 2], out[j + 3]);
+            }
+        } else {
+            for (uint32_t j = 0; j < cnt; ++j) dst[j] = out[j];
+        }
+    }
+#else
+    KeyT* row = stage + threadIdx.x * S::row;
+    KeyT* dst = keys + ts.base;
+#pragma unroll
+    for (int h = 0; h < kEB / S::keys; ++h) {
+        if (h) __syncthreads();   // the previous round's reads are done
+#pragma unroll
+        for (int j = 0; j < S::keys; j += 16 / (int)sizeof(KeyT)) {
+            const int o = h * S::keys + j;
+            if constexpr (sizeof(KeyT) == 8) *(ulonglong2*)(row + j) = make_ulonglong2(out[o], out[o + 1]);
+            else *(uint4*)(row + j) = make_uint4(out[o], out[o + 1], out[o + 2], out[o + 3]);
+        }
+        __syncthreads();
+        // staged key e = (thread r, key c) is slot r * kEB + h * S::keys + c of the tile
+#pragma unroll 4
+        for (uint32_t e = threadIdx.x; e < (uint32_t)T::emit_threads * S::keys; e += T::emit_threads) {
+            const uint32_t r = e / S::keys, c = e % S::keys, i = r * kEB + h * S::keys + c;
+            if (i < ts.cnt) dst[i] = stage[r * S::row + c];
+        }
+    }
+#endif
 }
 
 // ---- 2a. per-tile digit histogram (one row per digit: hist[d * hstride + t])
@@ -297,9 +355,15 @@ __global__ void __launch_bounds__(kSBlock) sp_hist_kernel(const KeyT* __restrict
     const uint32_t dmask = (1u << bits) - 1u;
     // order does not matter here: one LDS add per key into the wave's counters
     // (the ballot matching of the scatter costs ~60 VALU per 64 keys)
+    // every load first (a load per iteration, each waited for before its add,
+    // left the waves at HBM latency): indices clamped to the tile's last key
+    KeyT x[T::per];
+#pragma unroll
+    for (int it = 0; it < T::per; ++it) x[it] = keys[ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1)];
+#pragma unroll
     for (int it = 0; it < T::per; ++it) {
         const uint32_t li = w * T::wave_span + it * 64 + lane;
-        if (li < ts.cnt) atomicAdd(&wc[w][(uint32_t)(keys[ts.base + li] >> shift) & dmask], 1u);
+        if (li < ts.cnt) atomicAdd(&wc[w][(uint32_t)(x[it] >> shift) & dmask], 1u);
     }
     __syncthreads();
     if (tid <= (int)dmask) hist[(uint64_t)tid * hstride + blockIdx.x] = wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
@@ -350,10 +414,13 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
     const uint64_t lt = (1ull << lane) - 1;
     KeyT key[T::per];
     uint32_t rank[T::per];
+#pragma unroll
+    for (int it = 0; it < T::per; ++it) key[it] = in[ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1)];
+#pragma unroll
     for (int it = 0; it < T::per; ++it) {
         const uint32_t li = w * T::wave_span + it * 64 + lane;
         const bool v = li < ts.cnt;
-        const KeyT x = v ? in[ts.base + li] : (KeyT)0;
+        const KeyT x = key[it];
         const uint32_t d = (uint32_t)(x >> shift) & dmask;
 #if KF_SPARSE_RANK == 0
         const uint64_t m = match_digit(d, bits, __ballot(v));
@@ -365,7 +432,6 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
         (void)lt;
         rank[it] = v ? atomicAdd(&wc[w][d], 1u) : 0u;
 #endif
-        key[it] = x;
     }
     __syncthreads();
     {
@@ -400,23 +466,30 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
 
 // ---- 3a. run heads per tile (into hist row 0)
 template <typename KeyT>
-__device__ __forceinline__ bool is_head(const KeyT* keys, uint32_t p, uint32_t gs) {
-    return p == gs || keys[p] != keys[p - 1];
-}
-
-template <typename KeyT>
 __global__ void __launch_bounds__(kSBlock) sp_heads_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
                                                            uint32_t* tfirst, int n, uint32_t* heads) {
     using T = TileOf<KeyT>;
     __shared__ uint32_t wsum[kSWaves];
     TileSpan ts;
     if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // every load first (slot and predecessor; indices clamped into the tile / genome)
+    KeyT x[T::per], y[T::per];
+#pragma unroll
+    for (int it = 0; it < T::per; ++it) {
+        const uint32_t p = ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1);
+        x[it] = keys[p];
+        y[it] = keys[max(p, ts.gs + 1) - 1];
+    }
     uint32_t c = 0;
     bool disorder = false;
-    for (uint32_t i = threadIdx.x; i < ts.cnt; i += kSBlock) {
-        const uint32_t p = ts.base + i;
-        c += is_head(keys, p, ts.gs) ? 1u : 0u;
-        disorder |= p > ts.gs && keys[p] < keys[p - 1];
+#pragma unroll
+    for (int it = 0; it < T::per; ++it) {
+        const uint32_t li = w * T::wave_span + it * 64 + lane, p = ts.base + li;
+        if (li < ts.cnt) {
+            c += p == ts.gs || x[it] != y[it] ? 1u : 0u;
+            disorder |= p > ts.gs && x[it] < y[it];
+        }
     }
     if (__ballot(disorder) && (threadIdx.x & 63) == 0) atomicOr(&tfirst[n + 1], 2u);   // the sort's self-check
     for (int d = 32; d >= 1; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d, 64);
@@ -437,23 +510,35 @@ __global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restri
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt = (1ull << lane) - 1;
     uint32_t hm = 0, mine = 0;   // head flags of this lane's slots
-    for (int it = 0; it < T::per; ++it) {
-        const uint32_t li = w * T::wave_span + it * 64 + lane;
-        const bool h = li < ts.cnt && is_head(keys, ts.base + li, ts.gs);
-        hm |= (h ? 1u : 0u) << it;
-        mine += (uint32_t)__popcll(__ballot(h));
+    KeyT x[T::per];
+    {
+        KeyT y[T::per];
+#pragma unroll
+        for (int it = 0; it < T::per; ++it) {
+            const uint32_t p = ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1);
+            x[it] = keys[p];
+            y[it] = keys[max(p, ts.gs + 1) - 1];
+        }
+#pragma unroll
+        for (int it = 0; it < T::per; ++it) {
+            const uint32_t li = w * T::wave_span + it * 64 + lane, p = ts.base + li;
+            const bool h = li < ts.cnt && (p == ts.gs || x[it] != y[it]);
+            hm |= (h ? 1u : 0u) << it;
+            mine += (uint32_t)__popcll(__ballot(h));
+        }
     }
     if (lane == 0) wsum[w] = mine;
     __syncthreads();
     uint32_t u = heads[blockIdx.x];
     for (int x = 0; x < w; ++x) u += wsum[x];
+#pragma unroll
     for (int it = 0; it < T::per; ++it) {
         const bool h = (hm >> it) & 1u;
         const uint64_t b = __ballot(h);
         if (h) {
             const uint32_t li = w * T::wave_span + it * 64 + lane;
             const uint32_t j = u + (uint32_t)__popcll(b & lt);
-            ukeys[ts.gs + j] = (uint64_t)keys[ts.base + li];
+            ukeys[ts.gs + j] = (uint64_t)x[it];
             upos[ts.gs + j] = ts.base + li - ts.gs;
         }
         u += (uint32_t)__popcll(b);
@@ -461,18 +546,29 @@ __global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restri
 }
 
 // ---- 3c. counts = distance to the next head; tiles index unique slots here
+template <uint32_t Span>
 __global__ void __launch_bounds__(kSBlock) sp_counts_kernel(const uint64_t* goff, const uint32_t* tfirst, int n,
                                                             const uint32_t* nfull, const uint32_t* upos,
-                                                            uint32_t* __restrict__ counts, uint32_t span) {
+                                                            uint32_t* __restrict__ counts) {
+    constexpr int per = Span / kSBlock;
     TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, span)) return;
+    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, Span)) return;
     const uint32_t nf = nfull[ts.g * 256];
     const uint32_t len = ts.ge - ts.gs;
-    for (uint32_t i = threadIdx.x; i < ts.cnt; i += kSBlock) {
-        const uint32_t u = ts.base + i - ts.gs;
-        if (u >= nf) break;
-        const uint32_t nxt = u + 1 < nf ? upos[ts.gs + u + 1] : len;
-        counts[ts.gs + u] = nxt - upos[ts.gs + u];
+    const uint32_t u0 = ts.base - ts.gs;   // the tile's first unique index
+    if (u0 >= nf) return;
+    const uint32_t* up = upos + ts.gs;
+    uint32_t a[per], b[per];
+#pragma unroll
+    for (int it = 0; it < per; ++it) {   // every load first (indices clamped below nf)
+        const uint32_t u = min(u0 + it * kSBlock + threadIdx.x, nf - 1);
+        a[it] = up[u];
+        b[it] = up[min(u + 1, nf - 1)];
+    }
+#pragma unroll
+    for (int it = 0; it < per; ++it) {
+        const uint32_t i = it * kSBlock + threadIdx.x, u = u0 + i;
+        if (i < ts.cnt && u < nf) counts[ts.gs + u] = (u + 1 < nf ? b[it] : len) - a[it];
     }
 }
 
@@ -576,8 +672,8 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     hipLaunchKernelGGL(sp_scan_kernel, dim3((uint32_t)n, 1), dim3(kSBlock), 0, s, hist, L.hstride, tfirst, gtot);
     hipLaunchKernelGGL(sp_unique_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, kw, d_goff, tfirst, n, hist, d_keys,
                        upos);
-    hipLaunchKernelGGL(sp_counts_kernel, dim3(grid), dim3(kSBlock), 0, s, d_goff, tfirst, n, gtot, upos, d_counts,
-                       TileOf<KeyT>::tile);
+    hipLaunchKernelGGL(sp_counts_kernel<TileOf<KeyT>::tile>, dim3(grid), dim3(kSBlock), 0, s, d_goff, tfirst, n, gtot,
+                       upos, d_counts);
     const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
     hipLaunchKernelGGL(sp_nuniq_kernel<KeyT>, dim3((n + 255) / 256), dim3(256), 0, s, kw, d_goff, n, gtot, tfirst, sent,
                        d_nuniq);
