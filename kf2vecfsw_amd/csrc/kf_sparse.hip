@@ -12,10 +12,11 @@
 //              lexicographically smaller string), or SENT (= 4^k - 1, the code of
 //              T..T, never canonical) where no window ends;
 //   2. sort    each genome's keys, a segmented LSD radix sort of 2k bits in
-//              ceil(2k/8) passes of <= 8-bit digits: per pass a tile histogram,
-//              a per-(genome, digit) scan over the genome's tiles and a stable
-//              scatter (ranks by wave ballot matching, the tile re-ordered in LDS
-//              so every digit's keys leave as one contiguous run);
+//              ceil(2k/8) passes of equal <= 8-bit digits: one read counts every
+//              pass's digits per genome, then each pass is one single-sweep
+//              kernel (ranks by LDS atomics, the tile's digit offsets by
+//              decoupled look-back over the genome's earlier tiles, the tile
+//              re-ordered in LDS so every digit's keys leave as one run);
 //   3. unique  run heads of the sorted keys compacted with their positions; a
 //              run's count is the distance to the next head.  SENT sorts last and
 //              is dropped.
@@ -393,20 +394,112 @@ __global__ void __launch_bounds__(kSBlock) sp_scan_kernel(uint32_t* hist, uint32
 }
 
 // ---- 2c. stable scatter of one tile by digit
+// ---- 2'. single-sweep passes (KF_SPARSE_LOOKBACK = 1, the default): no tile
+// histogram pass and no scan.  The genome-wide digit counts of EVERY pass come
+// from one read of the emitted keys (sp_ghist_kernel); inside a pass, tile t
+// learns how many keys of digit d its genome's earlier tiles hold by decoupled
+// look-back: it publishes its own count (AGG), adds up its predecessors' words
+// back to the first inclusive prefix (INCL), then publishes its own INCL.  A
+// status word is (epoch << 34 | flag << 32 | count), one 64-bit store, so count
+// and flag are seen together; epoch = pass + 1 tells this pass's words from the
+// last pass's (the array is cleared once per call).  Tiles are numbered in the
+// order workgroups start (a ticket), so a tile only waits on tiles that are
+// already running; a wait that still exceeds ~2^22 polls flags the call (bit 2
+// of tfirst[n+1]: every count comes back UINT64_MAX - 1) instead of hanging.
+#ifndef KF_SPARSE_LOOKBACK
+#define KF_SPARSE_LOOKBACK 1
+#endif
+constexpr uint64_t kStAgg = 1, kStIncl = 2;
+
+__device__ __forceinline__ void st_publish(uint64_t* w, uint32_t epoch, uint64_t flag, uint32_t v) {
+    __hip_atomic_store(w, ((uint64_t)epoch << 34) | (flag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t lookback(uint64_t* status, uint32_t* tfirst, int n, uint32_t t, uint32_t t0,
+                                             uint32_t d, uint32_t tot, uint32_t epoch) {
+    uint64_t* mine = status + (uint64_t)t * 256 + d;
+    if (t == t0) {   // the genome's first tile: its prefix is its count
+        st_publish(mine, epoch, kStIncl, tot);
+        return 0;
+    }
+    st_publish(mine, epoch, kStAgg, tot);
+    uint32_t before = 0;
+    uint32_t spins = 0;
+    for (uint32_t j = t - 1;;) {
+        const uint64_t w = __hip_atomic_load(status + (uint64_t)j * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(w >> 34) != epoch) {   // not published yet
+            if (++spins > (1u << 22)) {
+                atomicOr(&tfirst[n + 1], 2u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        before += (uint32_t)w;
+        if (((w >> 32) & 3u) == kStIncl || j == t0) break;
+        --j;
+    }
+    st_publish(mine, epoch, kStIncl, before + tot);
+    return before;
+}
+
+// gall[(p * n + g) * 256 + d] += keys of genome g with digit d in pass p.
+// Workgroup (g, c) takes the c-th of gridDim.y slices of genome g.
 template <typename KeyT>
+__global__ void __launch_bounds__(kSBlock) sp_ghist_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
+                                                           const uint32_t* tfirst, int n, int passes, int bits,
+                                                           uint32_t* gall) {
+    __shared__ uint32_t cnt[8][256];
+    if (tfirst[n + 1] & 1u) return;   // invalid goff (sp_tiles_kernel): nothing is counted
+    const int g = blockIdx.x;
+    const uint32_t gs = (uint32_t)goff[g], len = (uint32_t)goff[g + 1] - gs;
+    const uint32_t part = (len + gridDim.y - 1) / gridDim.y;
+    const uint32_t c0 = gs + min(len, blockIdx.y * part), c1 = gs + min(len, (blockIdx.y + 1) * part);
+    if (c0 >= c1) return;
+    for (int i = threadIdx.x; i < passes * 256; i += kSBlock) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t dmask = (1u << bits) - 1u;   // digits above bit 2k are 0
+    constexpr int kB = 8;
+    for (uint32_t base = c0; base < c1; base += kSBlock * kB) {
+        KeyT x[kB];
+#pragma unroll
+        for (int j = 0; j < kB; ++j) x[j] = keys[min(base + j * kSBlock + threadIdx.x, c1 - 1)];
+#pragma unroll
+        for (int j = 0; j < kB; ++j) {
+            if (base + j * kSBlock + threadIdx.x < c1) {
+                for (int p = 0; p < passes; ++p) atomicAdd(&cnt[p][(uint32_t)(x[j] >> (p * bits)) & dmask], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < passes * 256; i += kSBlock) {
+        const uint32_t v = (&cnt[0][0])[i];
+        if (v) atomicAdd(&gall[((uint64_t)(i >> 8) * n + g) * 256 + (i & 255)], v);
+    }
+}
+
+template <typename KeyT, bool LB>
 __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restrict__ in, KeyT* __restrict__ out,
-                                                             const uint64_t* goff, const uint32_t* tfirst, int n,
+                                                             const uint64_t* goff, uint32_t* tfirst, int n,
                                                              int shift, int bits, const uint32_t* hist,
-                                                             uint32_t hstride, const uint32_t* gtot) {
+                                                             uint32_t hstride, const uint32_t* gtot,
+                                                             uint64_t* status, uint32_t* ticket, uint32_t epoch) {
     using T = TileOf<KeyT>;
     __shared__ uint32_t wc[kSWaves][256];   // per wave: digit counts, then the wave's base inside the digit
     __shared__ uint32_t lbase[256];         // tile-local start of each digit
     __shared__ uint32_t gdst[256];          // global slot of the digit's first key in this tile, minus lbase
     __shared__ uint32_t wsum[kSWaves];
+    __shared__ uint32_t tix;
     extern __shared__ __attribute__((aligned(16))) uint8_t sp_dyn[];
     KeyT* stage = (KeyT*)sp_dyn;   // T::tile keys (dynamic LDS: 32 KiB)
+    uint32_t t = blockIdx.x;
+    if constexpr (LB) {   // tiles in the order workgroups start: a tile only waits on started tiles
+        if (threadIdx.x == 0) tix = atomicAdd(ticket, 1u);
+        __syncthreads();
+        t = tix;
+    }
     TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
+    if (!tile_span(goff, tfirst, n, t, ts, T::tile)) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     for (int i = tid; i < kSWaves * 256; i += kSBlock) (&wc[0][0])[i] = 0;
     __syncthreads();
@@ -440,6 +533,12 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
         const bool live = d <= (int)dmask;
         const uint32_t tot = c0 + c1 + c2 + c3;
         const uint32_t gt = live ? gtot[ts.g * 256 + d] : 0u;
+        uint32_t before;   // keys of digit d in the genome's earlier tiles
+        if constexpr (LB) {
+            before = live ? lookback(status, tfirst, n, t, tfirst[ts.g], d, tot, epoch) : 0u;
+        } else {
+            before = live ? hist[(uint64_t)d * hstride + t] : 0u;
+        }
         const uint32_t lb = block_excl_scan(tot, wsum);
         const uint32_t gb = block_excl_scan(gt, wsum);
         wc[0][d] = 0;
@@ -447,7 +546,7 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
         wc[2][d] = c0 + c1;
         wc[3][d] = c0 + c1 + c2;
         lbase[d] = lb;
-        gdst[d] = live ? ts.gs + gb + hist[(uint64_t)d * hstride + blockIdx.x] - lb : 0u;
+        gdst[d] = live ? ts.gs + gb + before - lb : 0u;
     }
     __syncthreads();
     for (int it = 0; it < T::per; ++it) {
@@ -595,7 +694,7 @@ __global__ void __launch_bounds__(256) sp_nuniq_kernel(const KeyT* keys, const u
 
 // Workspace carve-up (byte offsets, 256-aligned).
 struct SpLayout {
-    uint64_t tfirst, keys, hist, gtot, upos, total;
+    uint64_t tfirst, keys, hist, gtot, upos, gall, ticket, total;   // hist doubles as the look-back status
     uint32_t hstride;
 };
 
@@ -611,11 +710,15 @@ SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
     L.keys = o;
     o = al256(o + ks * batch_bytes);
     L.hist = o;
-    o = al256(o + 4ull * 256 * L.hstride);
+    o = al256(o + (KF_SPARSE_LOOKBACK ? 8ull : 4ull) * 256 * L.hstride);
     L.gtot = o;
     o = al256(o + 4ull * 256 * (uint64_t)n);
     L.upos = o;
     o = al256(o + 4ull * batch_bytes);
+    L.gall = o;   // passes x n x 256 genome digit counts (look-back)
+    o = al256(o + 4ull * 8 * 256 * (uint64_t)n);
+    L.ticket = o;   // a tile counter per pass
+    o = al256(o + 4ull * 8);
     L.total = o;
     return L;
 }
@@ -624,7 +727,8 @@ template <typename KeyT>
 int sp_prepare() {   // the scatter's staging tile is dynamic LDS (64 KiB for u64 keys)
     static bool done = false;
     if (done) return KF_OK;
-    if (hipFuncSetAttribute((const void*)&sp_scatter_kernel<KeyT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)&sp_scatter_kernel<KeyT, KF_SPARSE_LOOKBACK != 0>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(TileOf<KeyT>::tile * sizeof(KeyT))) != hipSuccess)
         return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     done = true;
@@ -652,17 +756,32 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     KeyT* dst = (passes % 2 == 0) ? ka : kw;
     hipLaunchKernelGGL(sp_emit_kernel<KeyT>, dim3(grid), dim3(TileOf<KeyT>::emit_threads), 0, s, d_bytes, d_goff, tfirst, n, d_excl,
                        (uint32_t)n_excl, k, src);
+#if KF_SPARSE_LOOKBACK
+    uint64_t* status = (uint64_t*)(work + L.hist);
+    uint32_t* gall = (uint32_t*)(work + L.gall);
+    uint32_t* ticket = (uint32_t*)(work + L.ticket);
+    if (hipMemsetAsync(status, 0, 8ull * 256 * L.hstride, s) != hipSuccess ||
+        hipMemsetAsync(gall, 0, L.total - L.gall, s) != hipSuccess)   // gall and the tickets
+        return kf_fail(KF_EHIP, "memset failed");
+    const uint32_t slices = (uint32_t)max(1, min(1024, 4096 / max(1, (int)n)));
+    hipLaunchKernelGGL(sp_ghist_kernel<KeyT>, dim3((uint32_t)n, slices), dim3(kSBlock), 0, s, src, d_goff, tfirst, n,
+                       passes, bits, gall);
+#endif
     for (int p = 0; p < passes; ++p) {
         const int shift = p * bits;
         const int b = min(bits, bits_total - shift);
+#if KF_SPARSE_LOOKBACK
+        hipLaunchKernelGGL((sp_scatter_kernel<KeyT, true>), dim3(grid), dim3(kSBlock), TileOf<KeyT>::tile * sizeof(KeyT),
+                           s, src, dst, d_goff, tfirst, n, shift, b, nullptr, L.hstride,
+                           gall + (uint64_t)p * n * 256, status, ticket + p, (uint32_t)p + 1);
+#else
         hipLaunchKernelGGL(sp_hist_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, src, d_goff, tfirst, n, shift, b,
                            hist, L.hstride);
         hipLaunchKernelGGL(sp_scan_kernel, dim3((uint32_t)n, 1u << b), dim3(kSBlock), 0, s, hist, L.hstride, tfirst,
                            gtot);
-        hipLaunchKernelGGL(sp_scatter_kernel<KeyT>, dim3(grid), dim3(kSBlock), TileOf<KeyT>::tile * sizeof(KeyT), s,
-                           src, dst,
-                           d_goff, tfirst, n,
-                           shift, b, hist, L.hstride, gtot);
+        hipLaunchKernelGGL((sp_scatter_kernel<KeyT, false>), dim3(grid), dim3(kSBlock), TileOf<KeyT>::tile * sizeof(KeyT),
+                           s, src, dst, d_goff, tfirst, n, shift, b, hist, L.hstride, gtot, nullptr, nullptr, 0u);
+#endif
         KeyT* t = src;
         src = dst;
         dst = t;

@@ -1,28 +1,6 @@
 #!/bin/bash
-# round 4, calls 3+4: LDS microbench, full GPU suite (get_chunks rewrite, K1x for
-# k <= 6, u16 phase-2 halves), A/B vs the round-3 library for k <= 7 and u16 on/off for
-# k >= 10, get_chunks throughput, e2e CLI timeline, k=11 bucket profile + SQ counters
-set -o pipefail
-cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r04
-timeout -k 10 60 ./tools/bin/lds_ops > gpurun_out/r04/v4_lds_ops.txt 2>&1 &&
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
-    > gpurun_out/r04/v3_pytest_gpu.log 2>&1 &&
-for k in 3 5 6 7; do
-  timeout -k 10 200 python -u tools/lib_ab.py --libs tools/ab/libkf2vec_head.so,tools/ab/libkf2vec_new.so --k $k \
-      --rounds 4 --reps 5 > gpurun_out/r04/v3_lib_ab_k$k.json 2> gpurun_out/r04/v3_lib_ab_k$k.err || exit $?
-done &&
-for k in 11 12 10; do
-  timeout -k 10 200 python -u tools/lib_ab.py --libs tools/ab/libkf2vec_u16off.so,tools/ab/libkf2vec_new.so,tools/ab/libkf2vec_bperm.so --k $k \
-      --rounds 4 --reps 3 > gpurun_out/r04/v4_lib_ab_k${k}_u16.json 2> gpurun_out/r04/v4_lib_ab_k${k}_u16.err || exit $?
-done &&
-timeout -k 10 300 python -u tools/chunks_bench.py --genomes 32 --reps 3 > gpurun_out/r04/v3_chunks_bench.json 2> gpurun_out/r04/v3_chunks_bench.err &&
-timeout -k 10 200 python -u tools/r04_e2e_trace.py --parts 2,4,8,16 > gpurun_out/r04/v4_e2e_trace.json 2> gpurun_out/r04/v4_e2e_trace.err &&
-KF_BUCKET_PROFILE=1 KF2VEC_GPU_LIB=$GRAFT_REPO_ROOT/tools/ab/libkf2vec_prof.so timeout -k 10 120 python -u tools/r04_run.py --k 11 --reps 2 \
-    > gpurun_out/r04/v4_bucket_profile_k11.txt 2>&1 &&
-G1="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CU_CYCLES SQ_WAVES" &&
-G2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_ANY" &&
-LIB=tools/ab/libkf2vec_new.so K=11 TAG=r04/v4_pmc_k11_full GROUPS_LIST="$G1"$'\n'"$G2" bash tools/r04_pmc.sh &&
-LIB=tools/ab/libkf2vec_abl8.so K=11 TAG=r04/v4_pmc_k11_phase1 GROUPS_LIST="$G1"$'\n'"$G2" bash tools/r04_pmc.sh &&
-python3 tools/pmc_summary.py gpurun_out/r04/v4_pmc_k11_full bucket_kernel > gpurun_out/r04/v4_pmc_k11_full.txt &&
-python3 tools/pmc_summary.py gpurun_out/r04/v4_pmc_k11_phase1 bucket_kernel > gpurun_out/r04/v4_pmc_k11_phase1.txt
+# per-kernel breakdown of the sparse counter at k=31 and k=16 (u64 tile 4096)
+set -e
+mkdir -p gpurun_out/r04/v34_prof
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r04/v34_prof -o run -f csv -- python3 $GRAFT_REPO_ROOT/tools/sparse_bench.py --genomes 64 --k 16,31 --reps 2 > $GRAFT_REPO_ROOT/gpurun_out/r04/v34_sparse.json
