@@ -558,8 +558,9 @@ def sparse_bench(args, dev) -> dict:
             "roofline": {"bound": "hbm", "achieved": round(alg / (med * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBPS,
                          "unit": "GB/s", "frac": round(alg / (med * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
                          "alg_bytes_per_launch": alg,
-                         "design_bytes_per_launch": int(n * L * (1 + key_b + passes * 3 * key_b + 6 * key_b)),
-                         "note": f"LSD radix sort of {2 * k}-bit keys in {passes} passes of 3 x {key_b} B per key"},
+                         "design_bytes_per_launch": int(n * L * (1 + 2 * key_b + passes * 2 * key_b + 6 * key_b)),
+                         "note": f"LSD radix sort of {2 * k}-bit keys: emit, one digit count, {passes} single-sweep "
+                                 f"passes of 2 x {key_b} B per key, run-length encoding"},
             "parity": "ok" if ok else "MISMATCH"}
 
 

@@ -409,6 +409,12 @@ __global__ void __launch_bounds__(kSBlock) sp_scan_kernel(uint32_t* hist, uint32
 #ifndef KF_SPARSE_LOOKBACK
 #define KF_SPARSE_LOOKBACK 1
 #endif
+#ifndef KF_SPARSE_ABL   // profiling ablations of the scatter (tools/ builds; wrong order by design)
+#define KF_SPARSE_ABL 0
+#endif
+#ifndef KF_SPARSE_LBW   // predecessors read per look-back round trip
+#define KF_SPARSE_LBW 1   // 4 and 8 measured the same with the interleaved order (v39)
+#endif
 constexpr uint64_t kStAgg = 1, kStIncl = 2;
 
 __device__ __forceinline__ void st_publish(uint64_t* w, uint32_t epoch, uint64_t flag, uint32_t v) {
@@ -423,21 +429,38 @@ __device__ __forceinline__ uint32_t lookback(uint64_t* status, uint32_t* tfirst,
         return 0;
     }
     st_publish(mine, epoch, kStAgg, tot);
+    // KF_SPARSE_LBW predecessors per round trip (a status load goes past the
+    // XCD's L2: ~1-2 us), nearest first, summed up to the first inclusive word;
+    // a word not yet published ends the round there and is polled again
     uint32_t before = 0;
     uint32_t spins = 0;
-    for (uint32_t j = t - 1;;) {
-        const uint64_t w = __hip_atomic_load(status + (uint64_t)j * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(w >> 34) != epoch) {   // not published yet
+    uint32_t j = t - 1;   // nearest predecessor not yet added (>= t0)
+    for (;;) {
+        uint64_t w[KF_SPARSE_LBW];
+#pragma unroll
+        for (int q = 0; q < KF_SPARSE_LBW; ++q)
+            w[q] = __hip_atomic_load(status + (uint64_t)(j >= t0 + (uint32_t)q ? j - (uint32_t)q : t0) * 256 + d, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        bool done = false, stalled = false;
+#pragma unroll
+        for (int q = 0; q < KF_SPARSE_LBW; ++q) {
+            if (done || stalled) continue;
+            if ((uint32_t)(w[q] >> 34) != epoch) {   // not published yet
+                stalled = true;
+                continue;
+            }
+            before += (uint32_t)w[q];
+            if (((w[q] >> 32) & 3u) == kStIncl || j == t0) done = true;
+            else --j;
+        }
+        if (done) break;
+        if (stalled) {
             if (++spins > (1u << 22)) {
                 atomicOr(&tfirst[n + 1], 2u);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
-            continue;
         }
-        before += (uint32_t)w;
-        if (((w >> 32) & 3u) == kStIncl || j == t0) break;
-        --j;
     }
     st_publish(mine, epoch, kStIncl, before + tot);
     return before;
@@ -478,12 +501,34 @@ __global__ void __launch_bounds__(kSBlock) sp_ghist_kernel(const KeyT* __restric
     }
 }
 
+// Ticket -> tile for the single-sweep passes: tiles ordered by (index inside
+// the genome, genome), so the tiles running at once spread over the genomes'
+// independent look-back chains instead of queueing on one genome's chain.
+// Inside a genome the order is kept (what the look-back's progress needs).
+// O(n) per tile: used up to KF_SPARSE_ORDER_MAXN genomes (identity above).
+#ifndef KF_SPARSE_ORDER_MAXN
+#define KF_SPARSE_ORDER_MAXN 4096
+#endif
+__global__ void __launch_bounds__(kSBlock) sp_order_kernel(const uint32_t* tfirst, int n, uint32_t* order) {
+    const uint32_t t = blockIdx.x * kSBlock + threadIdx.x;
+    if (t >= tfirst[n]) return;
+    const int g = tile_genome(tfirst, n, t);
+    const uint32_t r = t - tfirst[g];
+    uint32_t pos = 0;
+    for (int h = 0; h < n; ++h) {
+        const uint32_t nt = tfirst[h + 1] - tfirst[h];
+        pos += min(nt, r) + (h < g && nt > r ? 1u : 0u);
+    }
+    order[pos] = t;
+}
+
 template <typename KeyT, bool LB>
 __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restrict__ in, KeyT* __restrict__ out,
                                                              const uint64_t* goff, uint32_t* tfirst, int n,
                                                              int shift, int bits, const uint32_t* hist,
                                                              uint32_t hstride, const uint32_t* gtot,
-                                                             uint64_t* status, uint32_t* ticket, uint32_t epoch) {
+                                                             uint64_t* status, uint32_t* ticket, uint32_t epoch,
+                                                             const uint32_t* order) {
     using T = TileOf<KeyT>;
     __shared__ uint32_t wc[kSWaves][256];   // per wave: digit counts, then the wave's base inside the digit
     __shared__ uint32_t lbase[256];         // tile-local start of each digit
@@ -494,7 +539,10 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
     KeyT* stage = (KeyT*)sp_dyn;   // T::tile keys (dynamic LDS: 32 KiB)
     uint32_t t = blockIdx.x;
     if constexpr (LB) {   // tiles in the order workgroups start: a tile only waits on started tiles
-        if (threadIdx.x == 0) tix = atomicAdd(ticket, 1u);
+        if (threadIdx.x == 0) {
+            const uint32_t x = atomicAdd(ticket, 1u);
+            tix = order && x < tfirst[n] ? order[x] : x;
+        }
         __syncthreads();
         t = tix;
     }
@@ -523,7 +571,12 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
         rank[it] = prior + r;
 #else
         (void)lt;
+#if KF_SPARSE_ABL == 3   // profiling only: no rank atomics
+        rank[it] = 0u;
+        if (v && lane == 0) wc[w][d] += 64u;
+#else
         rank[it] = v ? atomicAdd(&wc[w][d], 1u) : 0u;
+#endif
 #endif
     }
     __syncthreads();
@@ -535,7 +588,13 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
         const uint32_t gt = live ? gtot[ts.g * 256 + d] : 0u;
         uint32_t before;   // keys of digit d in the genome's earlier tiles
         if constexpr (LB) {
+#if KF_SPARSE_ABL == 1   // profiling only (wrong order): no look-back
+            before = 0u;
+            (void)status;
+            (void)epoch;
+#else
             before = live ? lookback(status, tfirst, n, t, tfirst[ts.g], d, tot, epoch) : 0u;
+#endif
         } else {
             before = live ? hist[(uint64_t)d * hstride + t] : 0u;
         }
@@ -559,6 +618,9 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
     __syncthreads();
     for (uint32_t i = tid; i < ts.cnt; i += kSBlock) {
         const KeyT x = stage[i];
+#if KF_SPARSE_ABL == 2   // profiling only: no global stores (one per tile)
+        if (i == 0)
+#endif
         out[gdst[(uint32_t)(x >> shift) & dmask] + i] = x;
     }
 }
@@ -694,7 +756,7 @@ __global__ void __launch_bounds__(256) sp_nuniq_kernel(const KeyT* keys, const u
 
 // Workspace carve-up (byte offsets, 256-aligned).
 struct SpLayout {
-    uint64_t tfirst, keys, hist, gtot, upos, gall, ticket, total;   // hist doubles as the look-back status
+    uint64_t tfirst, keys, hist, gtot, upos, gall, ticket, order, total;   // hist doubles as the look-back status
     uint32_t hstride;
 };
 
@@ -719,6 +781,8 @@ SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
     o = al256(o + 4ull * 8 * 256 * (uint64_t)n);
     L.ticket = o;   // a tile counter per pass
     o = al256(o + 4ull * 8);
+    L.order = o;    // ticket -> tile
+    o = al256(o + 4ull * L.hstride);
     L.total = o;
     return L;
 }
@@ -761,11 +825,16 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     uint32_t* gall = (uint32_t*)(work + L.gall);
     uint32_t* ticket = (uint32_t*)(work + L.ticket);
     if (hipMemsetAsync(status, 0, 8ull * 256 * L.hstride, s) != hipSuccess ||
-        hipMemsetAsync(gall, 0, L.total - L.gall, s) != hipSuccess)   // gall and the tickets
+        hipMemsetAsync(gall, 0, L.order - L.gall, s) != hipSuccess)   // gall and the tickets
         return kf_fail(KF_EHIP, "memset failed");
     const uint32_t slices = (uint32_t)max(1, min(1024, 4096 / max(1, (int)n)));
     hipLaunchKernelGGL(sp_ghist_kernel<KeyT>, dim3((uint32_t)n, slices), dim3(kSBlock), 0, s, src, d_goff, tfirst, n,
                        passes, bits, gall);
+    uint32_t* order = nullptr;
+    if (n > 1 && n <= KF_SPARSE_ORDER_MAXN) {
+        order = (uint32_t*)(work + L.order);
+        hipLaunchKernelGGL(sp_order_kernel, dim3((grid + kSBlock - 1) / kSBlock), dim3(kSBlock), 0, s, tfirst, n, order);
+    }
 #endif
     for (int p = 0; p < passes; ++p) {
         const int shift = p * bits;
@@ -773,14 +842,15 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
 #if KF_SPARSE_LOOKBACK
         hipLaunchKernelGGL((sp_scatter_kernel<KeyT, true>), dim3(grid), dim3(kSBlock), TileOf<KeyT>::tile * sizeof(KeyT),
                            s, src, dst, d_goff, tfirst, n, shift, b, nullptr, L.hstride,
-                           gall + (uint64_t)p * n * 256, status, ticket + p, (uint32_t)p + 1);
+                           gall + (uint64_t)p * n * 256, status, ticket + p, (uint32_t)p + 1, order);
 #else
         hipLaunchKernelGGL(sp_hist_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, src, d_goff, tfirst, n, shift, b,
                            hist, L.hstride);
         hipLaunchKernelGGL(sp_scan_kernel, dim3((uint32_t)n, 1u << b), dim3(kSBlock), 0, s, hist, L.hstride, tfirst,
                            gtot);
         hipLaunchKernelGGL((sp_scatter_kernel<KeyT, false>), dim3(grid), dim3(kSBlock), TileOf<KeyT>::tile * sizeof(KeyT),
-                           s, src, dst, d_goff, tfirst, n, shift, b, hist, L.hstride, gtot, nullptr, nullptr, 0u);
+                           s, src, dst, d_goff, tfirst, n, shift, b, hist, L.hstride, gtot, nullptr, nullptr, 0u,
+                           nullptr);
 #endif
         KeyT* t = src;
         src = dst;

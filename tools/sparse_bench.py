@@ -46,8 +46,11 @@ def main() -> None:
             if r:
                 ms.append(e0.elapsed_time(e1))
         nuh = nu.cpu().numpy()
-        g0 = sc.to_host(keys[: int(off[1])], cnts[: int(off[1])], nu[:1], off[:2])[0]
-        ok = int(g0[1].sum(dtype=np.uint64)) == a.seq_len - k + 1
+        try:
+            g0 = sc.to_host(keys[: int(off[1])], cnts[: int(off[1])], nu[:1], off[:2])[0]
+            ok = int(g0[1].sum(dtype=np.uint64)) == a.seq_len - k + 1
+        except Exception as e:   # profiling ablation builds (KF_SPARSE_ABL) sort wrongly by design
+            ok = f"no: {e}"
         med = float(np.median(ms))
         out["k"][k] = {"ms": round(med, 3), "ms_all": [round(x, 3) for x in ms],
                        "Gbases_s": round(bases / med / 1e6, 2),
