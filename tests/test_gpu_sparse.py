@@ -98,16 +98,36 @@ def test_sparse_equals_dense_rows(torch_dev, k):
 
 
 def test_sparse_tile_boundaries_and_many_genomes(torch_dev, oracle):
-    """Genome lengths around the tiles (2,048 slots for u64 keys, 8,192 for u32)
-    and 300 small genomes in one batch (many tiles, many segments per scan)."""
+    """Genome lengths around the tiles (4,096 slots for u64 keys, 8,192 for u32)
+    and 300 small genomes in one batch (many tiles, many look-back chains)."""
     rng = np.random.default_rng(9)
     blobs = []
-    for L in [1, 2046, 2047, 2048, 2049, 4095, 4096, 4097, 6143, 6145, 8191, 8192, 8193, 16383, 16385]:
+    for L in [1, 2046, 2047, 2048, 2049, 4095, 4096, 4097, 6143, 6145, 8191, 8192, 8193, 12289, 16383, 16385]:
         s = gen.random_seq(rng, L).tobytes()
         blobs.append(s[:L])
     blobs += [gen.random_fasta(rng, int(rng.integers(0, 3000))) for _ in range(300)]
     for k in (13, 31):
         check(oracle, blobs, k, run_sparse(blobs, k, torch_dev), tag=f"tiles k={k}")
+
+
+def test_sparse_ragged_tile_counts_interleaved_order(torch_dev, oracle):
+    """Genomes of 0 to ~60 tiles next to each other: the single-sweep passes
+    ticket tiles in (index in genome, genome) order, so short genomes drop out
+    of the rotation while long ones go on; one genome alone (no reordering)."""
+    rng = np.random.default_rng(77)
+    sizes = [0, 250_000, 1, 3000, 120_000, 0, 9000, 500_000, 17, 40_000]
+    blobs = [gen.random_seq(rng, L).tobytes()[:L] if L else b"" for L in sizes]
+    for k in (16, 31):
+        check(oracle, blobs, k, run_sparse(blobs, k, torch_dev), tag=f"ragged k={k}")
+        check(oracle, blobs[7:8], k, run_sparse(blobs[7:8], k, torch_dev), tag=f"single k={k}")
+
+
+def test_sparse_more_genomes_than_the_order_table(torch_dev, oracle):
+    """5,000 genomes in one batch (past KF_SPARSE_ORDER_MAXN = 4,096: tiles run
+    in plain order)."""
+    rng = np.random.default_rng(78)
+    blobs = [gen.random_seq(rng, int(L)).tobytes()[: int(L)] for L in rng.integers(0, 400, 5000)]
+    check(oracle, blobs, 21, run_sparse(blobs, 21, torch_dev), tag="n5000")
 
 
 def test_sparse_low_complexity_runs(torch_dev, oracle):
