@@ -84,10 +84,12 @@ struct TileSpan {
     uint32_t g, gs, ge, base, cnt;   // genome, its slot range, the tile's first slot and slot count
 };
 
+// tfirst[n + 2 + t] = the genome of tile t (sp_tilemap_kernel): one load
+// instead of a binary search's chain of dependent loads at every tile's start
 __device__ __forceinline__ bool tile_span(const uint64_t* goff, const uint32_t* tfirst, int n, uint32_t t,
                                           TileSpan& ts, uint32_t span) {
     if (t >= tfirst[n]) return false;
-    ts.g = (uint32_t)tile_genome(tfirst, n, t);
+    ts.g = tfirst[n + 2 + t];
     ts.gs = (uint32_t)goff[ts.g];
     ts.ge = (uint32_t)goff[ts.g + 1];
     ts.base = ts.gs + (t - tfirst[ts.g]) * span;
@@ -175,6 +177,29 @@ __global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, in
     }
 }
 
+// ---- tile map: tfirst[n + 2 + t] = genome of tile t; xlo[t] = the first
+// excluded range ending after the tile's first slot (xlo[tiles] = n_excl)
+__global__ void __launch_bounds__(256) sp_tilemap_kernel(const uint64_t* goff, uint32_t* tfirst, int n,
+                                                         const uint64_t* excl, uint32_t n_excl, uint32_t span,
+                                                         uint32_t* xlo) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x, nt = tfirst[n];
+    if (t > nt) return;
+    if (t == nt) {
+        xlo[t] = n_excl;
+        return;
+    }
+    const int g = tile_genome(tfirst, n, t);
+    tfirst[n + 2 + t] = (uint32_t)g;
+    const uint64_t base = goff[g] + (uint64_t)(t - tfirst[g]) * span;
+    uint32_t lo = 0, h = n_excl;
+    while (lo < h) {
+        const uint32_t m = (lo + h) >> 1;
+        if (excl[2 * m + 1] <= base) lo = m + 1;
+        else h = m;
+    }
+    xlo[t] = lo;
+}
+
 // ---- 1. emit: thread = kEB consecutive bytes of a tile; its k-1 bases
 // of context come from a walk back over the bytes before it (newlines skipped; a
 // break, an excluded range or the genome start ends the walk), then it rolls
@@ -198,7 +223,7 @@ struct EmitStage {
 // bytes at p0 = ts.base + threadIdx.x * kEB.
 template <typename KeyT>
 __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, const TileSpan& ts, uint32_t n_excl,
-                                         const uint64_t* excl, int k, KeyT (&out)[kEB]) {
+                                         const uint64_t* excl, const uint32_t* xlo, int k, KeyT (&out)[kEB]) {
     const uint32_t q0 = threadIdx.x * kEB;
     if (q0 >= ts.cnt) return;
     const uint32_t p0 = ts.base + q0, cnt = min((uint32_t)kEB, ts.cnt - q0);
@@ -225,7 +250,8 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
     // first excluded range ending after p0
     uint32_t ix = 0;
     {
-        uint32_t lo = 0, h = n_excl;
+        // the answer lies in [xlo[t], xlo[t + 1]] (sp_tilemap_kernel)
+        uint32_t lo = xlo[blockIdx.x], h = xlo[blockIdx.x + 1];
         while (lo < h) {
             const uint32_t m = (lo + h) >> 1;
             if (excl[2 * m + 1] <= p0) lo = m + 1;
@@ -291,7 +317,8 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
 template <typename KeyT>
 __global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
                                                             const uint32_t* tfirst, int n, const uint64_t* excl,
-                                                            uint32_t n_excl, int k, KeyT* __restrict__ keys) {
+                                                            uint32_t n_excl, const uint32_t* xlo, int k,
+                                                            KeyT* __restrict__ keys) {
     using T = TileOf<KeyT>;
     using S = EmitStage<KeyT>;
     __shared__ __attribute__((aligned(16))) KeyT stage[S::elems];
@@ -301,7 +328,7 @@ __global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(con
     KeyT out[kEB];
 #pragma unroll
     for (int j = 0; j < kEB; ++j) out[j] = sent;
-    emit_row(bytes, ts, n_excl, excl, k, out);
+    emit_row(bytes, ts, n_excl, excl, xlo, k, out);
 #if KF_SPARSE_EMIT == 0
     (void)stage;
     const uint32_t q0 = threadIdx.x * kEB;
@@ -512,7 +539,7 @@ __global__ void __launch_bounds__(kSBlock) sp_ghist_kernel(const KeyT* __restric
 __global__ void __launch_bounds__(kSBlock) sp_order_kernel(const uint32_t* tfirst, int n, uint32_t* order) {
     const uint32_t t = blockIdx.x * kSBlock + threadIdx.x;
     if (t >= tfirst[n]) return;
-    const int g = tile_genome(tfirst, n, t);
+    const int g = (int)tfirst[n + 2 + t];
     const uint32_t r = t - tfirst[g];
     uint32_t pos = 0;
     for (int h = 0; h < n; ++h) {
@@ -756,7 +783,7 @@ __global__ void __launch_bounds__(256) sp_nuniq_kernel(const KeyT* keys, const u
 
 // Workspace carve-up (byte offsets, 256-aligned).
 struct SpLayout {
-    uint64_t tfirst, keys, hist, gtot, upos, gall, ticket, order, total;   // hist doubles as the look-back status
+    uint64_t tfirst, xlo, keys, hist, gtot, upos, gall, ticket, order, total;   // hist doubles as the look-back status
     uint32_t hstride;
 };
 
@@ -767,8 +794,10 @@ SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
     const uint64_t ks = k <= 16 ? 4 : 8;
     L.hstride = (uint32_t)(batch_bytes / tile_for_k(k) + (uint64_t)n + 1);
     uint64_t o = 0;
-    L.tfirst = o;
-    o = al256(o + 4ull * ((uint64_t)n + 2));   // + the invalid-goff flag
+    L.tfirst = o;   // tfirst[0..n], the flags word, then the tile -> genome map
+    o = al256(o + 4ull * ((uint64_t)n + 2 + L.hstride));
+    L.xlo = o;
+    o = al256(o + 4ull * ((uint64_t)L.hstride + 1));
     L.keys = o;
     o = al256(o + ks * batch_bytes);
     L.hist = o;
@@ -815,11 +844,14 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     const int passes = (bits_total + 7) / 8;
     const int bits = (bits_total + passes - 1) / passes;
     hipLaunchKernelGGL(sp_tiles_kernel, dim3(1), dim3(1024), 0, s, d_goff, n, batch_bytes, TileOf<KeyT>::tile, tfirst);
+    uint32_t* xlo = (uint32_t*)(work + L.xlo);
+    hipLaunchKernelGGL(sp_tilemap_kernel, dim3(grid / 256 + 1), dim3(256), 0, s, d_goff, tfirst, n, d_excl,
+                       (uint32_t)n_excl, TileOf<KeyT>::tile, xlo);
     // the last pass must write kw: start in kw for an even number of passes
     KeyT* src = (passes % 2 == 0) ? kw : ka;
     KeyT* dst = (passes % 2 == 0) ? ka : kw;
     hipLaunchKernelGGL(sp_emit_kernel<KeyT>, dim3(grid), dim3(TileOf<KeyT>::emit_threads), 0, s, d_bytes, d_goff, tfirst, n, d_excl,
-                       (uint32_t)n_excl, k, src);
+                       (uint32_t)n_excl, xlo, k, src);
 #if KF_SPARSE_LOOKBACK
     uint64_t* status = (uint64_t*)(work + L.hist);
     uint32_t* gall = (uint32_t*)(work + L.gall);
