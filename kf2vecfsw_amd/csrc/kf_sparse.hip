@@ -227,7 +227,8 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
     const uint32_t q0 = threadIdx.x * kEB;
     if (q0 >= ts.cnt) return;
     const uint32_t p0 = ts.base + q0, cnt = min((uint32_t)kEB, ts.cnt - q0);
-    const uint64_t kmask = (1ull << (2 * k)) - 1;
+    using W = KeyT;   // window registers as wide as the key (2k <= 32 bits for u32 keys)
+    const W kmask = (W)((1ull << (2 * k)) - 1);
     const int hi = 2 * k - 2;
     uint32_t code[kEB];
     bool any = false;
@@ -262,7 +263,7 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
     // context: up to k-1 bases before p0 (most recent in the low pair)
     const uint64_t stop = ix > 0 ? excl[2 * ix - 1] : 0;   // end of the last excluded range before p0
     const uint64_t floor_ = max((uint64_t)ts.gs, stop);
-    uint64_t back = 0;
+    W back = 0;
     int m = 0;
     uint64_t q = p0;
     bool open = true;   // the walk may go on
@@ -276,7 +277,7 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
             const uint32_t c = sp_code((uint8_t)(wv[j >> 2] >> (8 * (j & 3))));
             if (open && m < k - 1 && c != 4) {
                 if (c == 5) open = false;
-                else back |= (uint64_t)c << (2 * m++);
+                else back |= (W)c << (2 * m++);
             }
         }
         q = p0 - kEB;
@@ -285,12 +286,12 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
         const uint32_t c = sp_code(bytes[--q]);
         if (c == 4) continue;
         if (c == 5) break;
-        back |= (uint64_t)c << (2 * m);
+        back |= (W)c << (2 * m);
         ++m;
     }
-    uint64_t fw = back, rc = 0;   // fw: the m context bases, most recent lowest
+    W fw = back, rc = 0;   // fw: the m context bases, most recent lowest
     int len = m;
-    for (int i = 0; i < m; ++i) rc |= (uint64_t)(3u - ((uint32_t)(back >> (2 * i)) & 3u)) << (hi - 2 * i);
+    for (int i = 0; i < m; ++i) rc |= (W)(3u - ((uint32_t)(back >> (2 * i)) & 3u)) << (hi - 2 * i);
     // the next excluded range's bounds (the thread's bytes rarely meet one)
     uint64_t xs = ix < n_excl ? excl[2 * ix] : ~0ull, xe = ix < n_excl ? excl[2 * ix + 1] : ~0ull;
 #pragma unroll
@@ -307,7 +308,7 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
                 len = 0;
             } else if (c < 4) {
                 fw = ((fw << 2) | c) & kmask;
-                rc = (rc >> 2) | ((uint64_t)(3u - c) << hi);
+                rc = (rc >> 2) | ((W)(3u - c) << hi);
                 if (++len >= k) out[j] = (KeyT)(fw < rc ? fw : rc);
             }
         }
