@@ -159,7 +159,9 @@ int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
  * offsets are checked on the device: if d_goff decreases or d_goff[n] >
  * batch_bytes, nothing is read or written and every d_nuniq[g] is UINT64_MAX.
  * The sorted keys are checked on the device too: a genome whose keys are not
- * in order makes every d_nuniq[g] UINT64_MAX - 1 (fail loudly, never silently). */
+ * in order, or a sort pass whose tile-to-tile prefix exchange (decoupled
+ * look-back) stalled past its bound, makes every d_nuniq[g] UINT64_MAX - 1
+ * (fail loudly, never silently or by hanging). */
 uint64_t kf_sparse_workspace_bytes(int k, uint64_t batch_bytes, int32_t n_genomes);
 int kf_sparse_count(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
                     uint64_t batch_bytes, const uint64_t* d_excl, uint64_t n_excl, int k,
