@@ -212,6 +212,35 @@ def test_features_handoff_equals_kf_text_round_trip(native, pseudo, raw):
         assert np.array_equal(got[i], exp, equal_nan=True), i
 
 
+def test_features_handoff_float32_equals_trainers_pandas_path(native):
+    """What the trainers feed their models is `torch.from_numpy(df.values *
+    1e4).float()` with df from my_read_csv (utils.py:436-437: pandas' DEFAULT
+    parser, not correctly rounded; train_model_set.py:291, 620).  counter.features
+    (...).float() equals that except where the parse's <= ~1e-12 relative error
+    crosses a float32 rounding boundary: there the two differ by one float32 ulp
+    (the hand-off's value is the correctly rounded one).  Bound: <= 1 ulp, in at
+    most 1 entry per 100,000 (measured: 1 of 786,432 here)."""
+    import io
+
+    import pandas as pd
+    import torch
+    from kf2vecfsw_amd import counter as C
+    from kf2vecfsw_amd.main import format_kf
+    rng = np.random.default_rng(23)
+    n_diff = n_all = 0
+    for t in range(48):
+        row = rng.integers(0, int(rng.choice([3, 50, 2000, 100000])), size=8192).astype(np.uint32)
+        for pseudo in (False, True):
+            got = C.features(torch.from_numpy(row[None].view(np.int32)), pseudo, False, scaler=1e4).float().numpy()[0]
+            df = pd.read_csv(io.BytesIO(format_kf(f"s{t}", row, pseudo)), index_col=0, header=None, sep=",")
+            exp = torch.from_numpy(df.values * 1e4).float().numpy()[0]
+            ulp = np.abs(got.view(np.int32).astype(np.int64) - exp.view(np.int32).astype(np.int64))
+            assert int(ulp.max()) <= 1, (t, pseudo)
+            n_diff += int(np.count_nonzero(ulp))
+            n_all += ulp.size
+    assert n_diff <= n_all // 100_000, (n_diff, n_all)
+
+
 def test_write_kf_segments_append_and_arenas(native, oracle, tmp_path):
     """kf_write_kf_segments (get_chunks' writer): several files at once, rows in
     order, a segment appended to the file an earlier call started, raw counts
