@@ -41,15 +41,20 @@ namespace {
 constexpr int kSBlock = 256;                   // threads per workgroup (4 waves)
 constexpr int kSWaves = kSBlock / 64;
 constexpr int kEB = 32;                        // emit: bytes per thread
-// Key slots per tile: 8192 u32 keys (32 keys per digit run on average; the
-// scatter stages 32 KiB) or 4096 u64 keys (16 per digit run: 128-byte runs; 2048
-// measured 3-9 % slower and 8192 4-18 % slower, profiles/r04/v28_*.json).
+// Key slots per tile: 16384 u32 keys or 8192 u64 keys (64 / 32 keys per 8-bit
+// digit run on average, 256-byte runs; the scatter stages 64 KiB).  With the
+// single-sweep passes fewer, larger tiles win despite 2-3 waves per SIMD
+// (profiles/r04/v49_*, v51_*: k = 31 17.1 -> 15.2 ms against u64 4096, k = 16
+// 7.14 -> 6.81 against u32 8192; u64 16384 is slower again, v50_*).
 template <typename KeyT>
 struct TileOf {
 #ifndef KF_SPARSE_TILE64   // u64 tile (tools/ A/B builds)
-#define KF_SPARSE_TILE64 4096
+#define KF_SPARSE_TILE64 8192
 #endif
-    static constexpr uint32_t tile = sizeof(KeyT) == 4 ? 8192u : (uint32_t)KF_SPARSE_TILE64;
+#ifndef KF_SPARSE_TILE32   // u32 tile (tools/ A/B builds)
+#define KF_SPARSE_TILE32 16384
+#endif
+    static constexpr uint32_t tile = sizeof(KeyT) == 4 ? (uint32_t)KF_SPARSE_TILE32 : (uint32_t)KF_SPARSE_TILE64;
     static constexpr int per = tile / kSBlock;             // slots per thread
     static constexpr uint32_t wave_span = tile / kSWaves;  // slots per wave
     static constexpr int emit_threads = tile / kEB;        // emit: kEB bytes per thread
@@ -698,7 +703,9 @@ __global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restri
     if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt = (1ull << lane) - 1;
-    uint32_t hm = 0, mine = 0;   // head flags of this lane's slots
+    static_assert(T::per <= 64, "head flags: one bit per slot of the lane");
+    uint64_t hm = 0;   // head flags of this lane's slots
+    uint32_t mine = 0;
     KeyT x[T::per];
     {
         KeyT y[T::per];
@@ -712,7 +719,7 @@ __global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restri
         for (int it = 0; it < T::per; ++it) {
             const uint32_t li = w * T::wave_span + it * 64 + lane, p = ts.base + li;
             const bool h = li < ts.cnt && (p == ts.gs || x[it] != y[it]);
-            hm |= (h ? 1u : 0u) << it;
+            hm |= (h ? 1ull : 0ull) << it;
             mine += (uint32_t)__popcll(__ballot(h));
         }
     }
