@@ -45,7 +45,7 @@ constexpr int kEB = 32;                        // emit: bytes per thread
 // digit run on average, 256-byte runs; the scatter stages 64 KiB).  With the
 // single-sweep passes fewer, larger tiles win despite 2-3 waves per SIMD
 // (profiles/r04/v49_*, v51_*: k = 31 17.1 -> 15.2 ms against u64 4096, k = 16
-// 7.14 -> 6.81 against u32 8192; u64 16384 is slower again, v50_*).
+// 7.14 -> 6.81 against u32 8192).
 template <typename KeyT>
 struct TileOf {
 #ifndef KF_SPARSE_TILE64   // u64 tile (tools/ A/B builds)
