@@ -658,6 +658,40 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
     }
 }
 
+// The key before slot li of the wave-span layout (li = w * wave_span + it * 64 +
+// lane): lane - 1 of the same load, lane 63 of the previous one, or for the
+// wave's first slot one extra (wave-uniform) load -- one key load per slot
+// instead of two.
+template <typename KeyT>
+__device__ __forceinline__ KeyT wave_shfl(KeyT v, int src, bool up) {
+    if constexpr (sizeof(KeyT) == 8) {
+        const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+        const uint32_t l = (uint32_t)(up ? __shfl_up((int)lo, 1, 64) : __shfl((int)lo, src, 64));
+        const uint32_t h = (uint32_t)(up ? __shfl_up((int)hi, 1, 64) : __shfl((int)hi, src, 64));
+        return ((KeyT)h << 32) | l;
+    } else {
+        return (KeyT)(up ? __shfl_up((int)v, 1, 64) : __shfl((int)v, src, 64));
+    }
+}
+
+// every key of the lane first; returns the key before the wave's first slot
+template <typename KeyT>
+__device__ __forceinline__ KeyT load_keys(const KeyT* __restrict__ keys, const TileSpan& ts, int w, int lane,
+                                          KeyT (&x)[TileOf<KeyT>::per]) {
+    using T = TileOf<KeyT>;
+#pragma unroll
+    for (int it = 0; it < T::per; ++it) x[it] = keys[ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1)];
+    const uint32_t p0 = ts.base + min(w * T::wave_span, ts.cnt - 1);
+    return keys[max(p0, ts.gs + 1) - 1];   // unused when p0 == gs (a head)
+}
+
+template <typename KeyT>
+__device__ __forceinline__ KeyT prev_key(const KeyT (&x)[TileOf<KeyT>::per], int it, int lane, KeyT first_prev) {
+    const KeyT up = wave_shfl(x[it], 0, true);
+    const KeyT last = it ? wave_shfl(x[it > 0 ? it - 1 : 0], 63, false) : first_prev;
+    return lane ? up : last;
+}
+
 // ---- 3a. run heads per tile (into hist row 0)
 template <typename KeyT>
 __global__ void __launch_bounds__(kSBlock) sp_heads_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
@@ -668,21 +702,17 @@ __global__ void __launch_bounds__(kSBlock) sp_heads_kernel(const KeyT* __restric
     if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // every load first (slot and predecessor; indices clamped into the tile / genome)
-    KeyT x[T::per], y[T::per];
-#pragma unroll
-    for (int it = 0; it < T::per; ++it) {
-        const uint32_t p = ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1);
-        x[it] = keys[p];
-        y[it] = keys[max(p, ts.gs + 1) - 1];
-    }
+    KeyT x[T::per];
+    const KeyT fp = load_keys(keys, ts, w, lane, x);
     uint32_t c = 0;
     bool disorder = false;
 #pragma unroll
     for (int it = 0; it < T::per; ++it) {
         const uint32_t li = w * T::wave_span + it * 64 + lane, p = ts.base + li;
+        const KeyT y = prev_key(x, it, lane, fp);
         if (li < ts.cnt) {
-            c += p == ts.gs || x[it] != y[it] ? 1u : 0u;
-            disorder |= p > ts.gs && x[it] < y[it];
+            c += p == ts.gs || x[it] != y ? 1u : 0u;
+            disorder |= p > ts.gs && x[it] < y;
         }
     }
     if (__ballot(disorder) && (threadIdx.x & 63) == 0) atomicOr(&tfirst[n + 1], 2u);   // the sort's self-check
@@ -708,17 +738,12 @@ __global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restri
     uint32_t mine = 0;
     KeyT x[T::per];
     {
-        KeyT y[T::per];
-#pragma unroll
-        for (int it = 0; it < T::per; ++it) {
-            const uint32_t p = ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1);
-            x[it] = keys[p];
-            y[it] = keys[max(p, ts.gs + 1) - 1];
-        }
+        const KeyT fp = load_keys(keys, ts, w, lane, x);
 #pragma unroll
         for (int it = 0; it < T::per; ++it) {
             const uint32_t li = w * T::wave_span + it * 64 + lane, p = ts.base + li;
-            const bool h = li < ts.cnt && (p == ts.gs || x[it] != y[it]);
+            const KeyT y = prev_key(x, it, lane, fp);
+            const bool h = li < ts.cnt && (p == ts.gs || x[it] != y);
             hm |= (h ? 1ull : 0ull) << it;
             mine += (uint32_t)__popcll(__ballot(h));
         }
