@@ -63,14 +63,15 @@ struct TileOf {
 constexpr uint32_t tile_for_k(int k) { return k <= 16 ? TileOf<uint32_t>::tile : TileOf<uint64_t>::tile; }
 
 // Standard 2-bit code of a byte: A0 C1 G2 T3 (either case), 4 = '\n', 5 = other.
+// Branch-free (a switch compiled to a compare tree with exec-mask branches per
+// byte): u = c | 0x20 is a, c, g or t only for those letters in either case
+// (bit 5 is the only case bit), bits 0, 2, 6, 19 of 0x80045 mark them, and
+// x = (u >> 1) & 3 is a0 c1 g3 t2, so x ^ (x >> 1) is the standard code.
 __device__ __forceinline__ uint32_t sp_code(uint8_t c) {
-    switch (c | 0x20) {
-    case 'a': return 0;
-    case 'c': return 1;
-    case 'g': return 2;
-    case 't': return 3;
-    default: return c == '\n' ? 4u : 5u;
-    }
+    const uint32_t u = (uint32_t)c | 0x20u, i = u - (uint32_t)'a';
+    const bool base = i < 26u && ((0x80045u >> i) & 1u);
+    const uint32_t x = (u >> 1) & 3u;
+    return base ? (x ^ (x >> 1)) : (c == '\n' ? 4u : 5u);
 }
 
 // Genome of tile t (t < tfirst[n]): the last g with tfirst[g] <= t (empty
@@ -299,6 +300,21 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
     for (int i = 0; i < m; ++i) rc |= (W)(3u - ((uint32_t)(back >> (2 * i)) & 3u)) << (hi - 2 * i);
     // the next excluded range's bounds (the thread's bytes rarely meet one)
     uint64_t xs = ix < n_excl ? excl[2 * ix] : ~0ull, xe = ix < n_excl ? excl[2 * ix + 1] : ~0ull;
+    // one step of the window, without branches: a base rolls in, '\n' (4) is
+    // transparent, anything else (5) breaks the window
+    auto roll = [&](int j, uint32_t c) {
+        const bool isb = c < 4u;
+        const uint32_t cb = c & 3u;
+        fw = isb ? (W)(((fw << 2) | cb) & kmask) : fw;
+        rc = isb ? (W)((rc >> 2) | ((W)(3u - cb) << hi)) : rc;
+        len = c == 5u ? 0 : len + (isb ? 1 : 0);
+        out[j] = isb && len >= k ? (KeyT)(fw < rc ? fw : rc) : out[j];
+    };
+    if (xs >= (uint64_t)p0 + kEB) {   // no excluded byte here (bytes past cnt hold code 4)
+#pragma unroll
+        for (int j = 0; j < kEB; ++j) roll(j, code[j]);
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < kEB; ++j) {
         const uint32_t p = p0 + j;
@@ -308,14 +324,7 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
                 xs = ix < n_excl ? excl[2 * ix] : ~0ull;
                 xe = ix < n_excl ? excl[2 * ix + 1] : ~0ull;
             }
-            const uint32_t c = p >= xs ? 5u : code[j];
-            if (c == 5) {
-                len = 0;
-            } else if (c < 4) {
-                fw = ((fw << 2) | c) & kmask;
-                rc = (rc >> 2) | ((W)(3u - c) << hi);
-                if (++len >= k) out[j] = (KeyT)(fw < rc ? fw : rc);
-            }
+            roll(j, p >= xs ? 5u : code[j]);
         }
     }
 }
