@@ -40,7 +40,9 @@ present canonical k-mers per genome by a device radix sort) on 64 of the
 synthetic genomes, genome 0 checked against the oracle.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--k 7]
-  (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+  (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...,
+   or plain `python bench.py --gpus N`: the process then starts N ranks itself,
+   one per GPU, before it touches the GPU, and relays rank 0's line)
 """
 from __future__ import annotations
 
@@ -65,7 +67,9 @@ SUB_BATCH = 6_250                 # genomes per resident sub-batch (the N=8 shar
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE under torchrun, else 1.  Without torchrun "
+                         "N > 1 starts N rank processes here")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--k", type=int, default=7)
@@ -564,13 +568,95 @@ def sparse_bench(args, dev) -> dict:
             "parity": "ok" if ok else "MISMATCH"}
 
 
+def resolve_world(args, env=None) -> tuple[int, bool]:
+    """(world size, spawn here?) from --gpus and the launcher's WORLD_SIZE.
+    Under a launcher (WORLD_SIZE set) --gpus must match it; without one,
+    --gpus N > 1 means this process starts the N ranks itself.  Raises
+    SystemExit with a message on a mismatch -- a scaling run must never time
+    fewer GPUs than it names."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        ws = int(ws)
+        if args.gpus is not None and args.gpus != ws:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (the launcher started {ws} "
+                             f"rank(s)); refusing to time a different number of GPUs than named")
+        return ws, False
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}: need at least one GPU")
+    return n, n > 1
+
+
+def spawn_ranks(n: int, argv: list[str], env=None) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1) -- exactly
+    what torch.distributed.run would give them -- and relay rank 0's stdout.
+    This process never touches the GPU (no HIP call before the children start;
+    no exec).  If a rank fails, the others get 60 s to finish, then are
+    terminated by PID.  Returns the worst exit status (0 if all ranks passed)."""
+    import socket
+    import subprocess
+    import threading
+    env = dict(os.environ if env is None else env)
+    from kf2vecfsw_amd.main import visible_gpus   # KFD topology / *_VISIBLE_DEVICES, no HIP init
+    avail = visible_gpus()
+    if env.get("KF_BENCH_REHEARSE") != "1" and avail is not None and n > avail:
+        print(f"bench.py: --gpus {n} but only {avail} GPU(s) visible", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KF_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=e,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+
+    def relay():
+        for line in procs[0].stdout:
+            sys.stdout.write(line.decode(errors="replace"))
+            sys.stdout.flush()
+
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    deadline = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            break
+        if deadline is None and any(rc not in (None, 0) for rc in rcs):
+            deadline = time.monotonic() + 60.0
+        if deadline is not None and time.monotonic() > deadline:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    t.join(timeout=10)
+    rcs = [p.wait() for p in procs]
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc]
+    if bad:
+        print("bench.py: rank(s) failed: " + ", ".join(f"rank {r} exit {rc}" for r, rc in bad), file=sys.stderr)
+        return max(abs(rc) for _, rc in bad) or 1
+    return 0
+
+
 def main() -> None:
     args = parse_args()
+    world, spawn = resolve_world(args)
+    if spawn:
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knob: KF_BENCH_REHEARSE=1 runs every rank on cuda:0 over gloo (one
@@ -673,7 +759,16 @@ def main() -> None:
                     if ceiling else None),
         "parity": "ok" if ok else "MISMATCH",
         "build_id": N.build_id(),
+        "ranks": {"world_size_reported": dist.get_world_size() if world > 1 else 1,
+                  "backend": (dist.get_backend() if world > 1 else None),
+                  "launcher": ("bench.py --gpus (spawned ranks)" if os.environ.get("KF_BENCH_SPAWNED")
+                               else "torch.distributed.run" if world > 1 else "single process"),
+                  "devices": ("cuda:0 for every rank (KF_BENCH_REHEARSE)" if rehearse
+                              else f"cuda:LOCAL_RANK, {world} GPU(s)")},
     }
+    if out["ranks"]["world_size_reported"] != world:
+        ok = False
+        out["parity"] = "MISMATCH"
     if args.secondary_k and world == 1 and args.secondary_k != args.k and resident:
         k2 = args.secondary_k
         st2 = max(3, args.steps // 4)

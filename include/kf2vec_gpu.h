@@ -154,7 +154,8 @@ int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
  * goff[g] distinct k-mers, so both arrays hold batch_bytes = goff[n] entries).
  * The device sorts the windows' keys (segmented LSD radix sort of 2k bits) in
  * d_work, which must hold kf_sparse_workspace_bytes(k, batch_bytes, n_genomes)
- * bytes; d_keys is also used as sort scratch.  batch_bytes < 2^32.
+ * bytes; d_keys is also used as sort scratch.  batch_bytes < 2^32 and d_bytes
+ * 16-byte aligned (KF_EINVAL otherwise, as kf_count_batch).
  * Asynchronous on `stream`, no allocation, no host synchronisation.  The
  * offsets are checked on the device: if d_goff decreases or d_goff[n] >
  * batch_bytes, nothing is read or written and every d_nuniq[g] is UINT64_MAX.

@@ -91,9 +91,13 @@ def lib() -> ctypes.CDLL:
         if L.kf_abi_version() != 1:
             raise NativeError("libkf2vec_gpu ABI version mismatch")
         bid = L.kf_build_id().decode()
-        if not os.environ.get("KF2VEC_GPU_LIB"):
-            # the product library must be built from the sources next to it
-            # (it travels prebuilt with repo snapshots; build.source_id)
+        # Any library must be built from the sources next to it (it travels
+        # prebuilt with repo snapshots; build.source_id), whether it is the
+        # product path or KF2VEC_GPU_LIB -- except a build that says it differs:
+        # a "+prof" / "+flags..." / "+zoo" suffix (profiling, ablation and zoo
+        # builds for tools/), or a library from another commit that an A/B tool
+        # loads on purpose (KF2VEC_ALLOW_FOREIGN_LIB=1).
+        if "+" not in bid and os.environ.get("KF2VEC_ALLOW_FOREIGN_LIB") != "1":
             from .build import source_id
             if bid != source_id():
                 raise NativeError(f"{LIB_PATH} was built from other sources (build id {bid}, sources "

@@ -126,8 +126,8 @@ def build_zoo() -> str:
                        + os.environ.get("KF_HIPCC_FLAGS", "").split(), check=True)
         objs.append(o)
     o = os.path.join(bld, "kf_host.cpp.o")
-    subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", "-c", os.path.join(CSRC, "kf_host.cpp"), "-o", o],
-                   check=True)
+    subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", f'-DKF_BUILD_ID="{source_id()}+zoo"',
+                    "-c", os.path.join(CSRC, "kf_host.cpp"), "-o", o], check=True)
     objs.append(o)
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs, "-o", out], check=True)
     return out

@@ -201,7 +201,10 @@ def index_on_device(data: torch.Tensor, off: torch.Tensor, n: int, nbytes: int) 
     nb = (nbytes + 4095) // 4096
     scratch = torch.empty(nb + 1, dtype=torch.int32, device=dev)
     npairs = torch.zeros(1, dtype=torch.int64, device=dev)
-    cap = nbytes // 64 + 16 * n + 1024   # a header every 64 bytes; more is re-run
+    # 64 header lines per genome to start (draft assemblies with more contigs
+    # re-run once with the exact count; ADVICE r04: a bytes-proportional first
+    # guess allocated ~25 % of the batch)
+    cap = 64 * n + 4096
     while True:
         excl = torch.empty(max(2 * cap, 2), dtype=torch.int64, device=dev)
         N.check(N.lib().kf_index_fasta(data.data_ptr(), off.data_ptr(), n, nbytes, excl.data_ptr(), cap,
@@ -322,11 +325,13 @@ class SparseCounter:
     def workspace_bytes(self, batch_bytes: int, n: int) -> int:
         return int(N.lib().kf_sparse_workspace_bytes(self.k, int(batch_bytes), int(n)))
 
-    def count(self, db: DeviceBatch, batch_bytes: int, stream: int | None = None):
+    def count(self, db: DeviceBatch, batch_bytes: int):
         """Enqueue the sparse count of a batch whose genomes end at batch_bytes
-        (= off[n]); returns (keys int64[batch_bytes] holding uint64 codes,
-        counts int32[batch_bytes] holding uint32, nuniq int64[n]) on the device:
-        genome g's k-mers are keys[off[g] : off[g] + nuniq[g]]."""
+        (= off[n]) on the current stream (the outputs and the reused workspace
+        belong to that stream's allocator pool, so there is no stream argument);
+        returns (keys int64[batch_bytes] holding uint64 codes, counts
+        int32[batch_bytes] holding uint32, nuniq int64[n]) on the device: genome
+        g's k-mers are keys[off[g] : off[g] + nuniq[g]]."""
         batch_bytes = int(batch_bytes)
         need = self.workspace_bytes(batch_bytes, db.n)
         if self._work is None or self._work.numel() < need:
@@ -335,7 +340,7 @@ class SparseCounter:
         keys = torch.empty(max(batch_bytes, 1), dtype=torch.int64, device=self.device)
         counts = torch.empty(max(batch_bytes, 1), dtype=torch.int32, device=self.device)
         nuniq = torch.zeros(max(db.n, 1), dtype=torch.int64, device=self.device)
-        s = _stream_ptr(self.device) if stream is None else stream
+        s = _stream_ptr(self.device)
         with torch.cuda.device(self.device):
             N.check(N.lib().kf_sparse_count(
                 db.data.data_ptr(), db.off.data_ptr(), db.n, batch_bytes,

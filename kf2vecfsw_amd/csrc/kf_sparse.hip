@@ -965,6 +965,8 @@ extern "C" int kf_sparse_count(const uint8_t* d_bytes, const uint64_t* d_goff, i
     if (n_excl >= (1ull << 31)) return kf_fail(KF_EINVAL, "too many excluded ranges");
     if (!d_bytes || !d_goff || (n_excl && !d_excl) || !d_work || !d_keys || !d_counts || !d_nuniq)
         return kf_fail(KF_EINVAL, "null device pointer");
+    if ((uintptr_t)d_bytes & 15u)   // as kf_count_batch: the emit's 16-byte loads assume it
+        return kf_fail(KF_EINVAL, "d_bytes must be 16-byte aligned");
     const SpLayout L = sp_layout(k, batch_bytes, n_genomes);
     if (work_bytes < L.total)
         return kf_fail(KF_ERANGE, "workspace needs %llu bytes (kf_sparse_workspace_bytes)",

@@ -56,6 +56,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_synth_header_len.argtypes = [ctypes.c_int64]
         L.oracle_synth_genome.argtypes = [ctypes.c_int64, u64, u64, i32, u64, vp, u64]
         L.oracle_sparse_count.argtypes = [vp, u64, i32, i32, vp, vp, vp]
+        L.oracle_sparse_count_many.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, i32]
         _lib = L
     return _lib
 
@@ -257,6 +258,22 @@ def sparse_count(data: bytes | np.ndarray, k: int, fmt: int = 0) -> tuple[np.nda
     n = ctypes.c_uint64(0)
     assert lib().oracle_sparse_count(_ptr(a), a.size, k, fmt, _ptr(keys), _ptr(cnt), ctypes.byref(n)) == 0
     return keys[: n.value].copy(), cnt[: n.value].copy()
+
+
+def sparse_count_many(buf: np.ndarray, off: np.ndarray, k: int, fmt: int = 0, threads: int = 0):
+    """sparse_count of every genome of a packed batch (OpenMP over genomes), in
+    the device counter's layout: (keys uint64[off[n]], counts uint32[off[n]],
+    nuniq uint64[n]) with genome g's k-mers at [off[g], off[g] + nuniq[g])."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    n = off.size - 1
+    tot = max(int(off[-1]), 1)
+    keys = np.zeros(tot, dtype=np.uint64)
+    cnt = np.zeros(tot, dtype=np.uint32)
+    nu = np.zeros(max(n, 1), dtype=np.uint64)
+    assert lib().oracle_sparse_count_many(_ptr(buf), _ptr(off), n, k, fmt, _ptr(keys), _ptr(cnt), _ptr(nu),
+                                          threads) == 0
+    return keys, cnt, nu[:n]
 
 
 def std_code_text(keys: np.ndarray, k: int) -> list[str]:

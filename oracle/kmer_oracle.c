@@ -340,6 +340,30 @@ int oracle_sparse_count(const uint8_t* bytes, uint64_t len, int k, int fmt, uint
     return 0;
 }
 
+/* oracle_sparse_count over many genomes (genome g = bytes[off[g], off[g+1])),
+ * OpenMP over genomes, in the device counter's layout: genome g's present
+ * k-mers at keys[off[g] ...] / counts[off[g] ...], their number in nuniq[g]
+ * (keys and counts hold off[n] entries).  For the full-size GPU parity test. */
+int oracle_sparse_count_many(const uint8_t* bytes, const uint64_t* off, int n_genomes, int k, int fmt,
+                             uint64_t* keys, uint32_t* counts, uint64_t* nuniq, int n_threads) {
+    if (k < 1 || k > 31) return -1;
+    int rc = 0;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int g = 0; g < n_genomes; ++g) {
+        if (oracle_sparse_count(bytes + off[g], off[g + 1] - off[g], k, fmt, keys + off[g], counts + off[g],
+                                nuniq + g) != 0) {
+#ifdef _OPENMP
+#pragma omp atomic write
+#endif
+            rc = -1;
+        }
+    }
+    return rc;
+}
+
 int oracle_max_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

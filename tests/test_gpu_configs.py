@@ -93,3 +93,70 @@ def test_configs3_shard_path(torch_dev, oracle, resident, rank, world):
     assert m["ok"]
     assert len(m["launch_ms"]) == 2 * W.nsb
     assert m["el"] > 0
+
+
+@pytest.mark.parametrize("n_period", [0, 3])
+def test_configs4_full_batch_every_genome(torch_dev, oracle, n_period):
+    """BASELINE configs[4]: k=11 (4^11 codes, 2,098,176 columns: the bucket kernel,
+    bins far beyond the LDS) over the same 1,000 x 5 Mbp device-generated batch as
+    the bench, every genome's row and total bit-exact against the oracle
+    (kf2vec/main.py:291-296 is the reference's large-k vocab branch; the counts
+    are Jellyfish's, main.py:309-323).  The rows are compared 100 genomes at a
+    time so the host holds ~1 GB of each side at once."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    n, L, k = 1000, 5_000_000, 11
+    db = C.synth_device_batch(n, L, SEED, width=80, n_period=n_period, device=torch_dev)
+    kc = C.KmerCounter(k, torch_dev)
+    cnt, tot = kc.count(db)
+    torch.cuda.synchronize()
+    totals = tot.cpu().numpy()
+    off = db.off.cpu().numpy().view(np.uint64)
+    host = db.data.cpu().numpy()
+    del db
+    if n_period == 0:
+        assert (totals == L - k + 1).all()
+    else:
+        assert (totals < L - k + 1).all() and (totals > L // 2).all()
+    threads = host_threads()
+    step = 100
+    for g0 in range(0, n, step):
+        g1 = min(n, g0 + step)
+        sub = off[g0: g1 + 1] - off[g0]
+        oc, ot = oracle.count_many_parts(host[int(off[g0]): int(off[g1])], sub, k, 1, threads, 4 << 20)
+        assert np.array_equal(ot, totals[g0:g1]), g0
+        got = C.counts_to_numpy(cnt[g0:g1])
+        bad = np.nonzero((oc != got).any(axis=1))[0]
+        assert bad.size == 0, f"k=11: {bad.size} genomes differ, e.g. {(bad[:8] + g0).tolist()}"
+        del oc, got
+    del cnt, tot
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("k", [16, 31])
+def test_sparse_bench_size_every_genome(torch_dev, oracle, k):
+    """bench.py's `sparse` workload at its own size: 64 x 5 Mbp device-generated
+    genomes (324 M keys), every genome's present canonical k-mers and counts
+    bit-exact against the oracle's sort-based restatement (OpenMP over genomes);
+    k=16 is the u32-key path, k=31 the u64 one (get_kmers, kf2vec/main.py:133-172)."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    n, L = 64, 5_000_000
+    db = C.synth_device_batch(n, L, SEED, width=80, device=torch_dev)
+    off = C.synth_layout(n, L)
+    sc = C.SparseCounter(k, torch_dev)
+    keys, cnts, nu = sc.count(db, int(off[-1]))
+    torch.cuda.synchronize()
+    gk = keys.cpu().numpy().view(np.uint64)
+    gc = cnts.cpu().numpy().view(np.uint32)
+    gn = nu.cpu().numpy().view(np.uint64)
+    host = db.data.cpu().numpy()
+    del keys, cnts, nu, db, sc
+    torch.cuda.empty_cache()
+    ek, ec, en = oracle.sparse_count_many(host[: int(off[-1])], off, k, 1, host_threads())
+    assert np.array_equal(gn, en)
+    for g in range(n):
+        a, m = int(off[g]), int(en[g])
+        assert np.array_equal(gk[a: a + m], ek[a: a + m]), (k, g)
+        assert np.array_equal(gc[a: a + m], ec[a: a + m]), (k, g)
+        assert int(ec[a: a + m].sum(dtype=np.uint64)) == L - k + 1

@@ -98,8 +98,9 @@ def test_sparse_equals_dense_rows(torch_dev, k):
 
 
 def test_sparse_tile_boundaries_and_many_genomes(torch_dev, oracle):
-    """Genome lengths around the tiles (4,096 slots for u64 keys, 8,192 for u32)
-    and 300 small genomes in one batch (many tiles, many look-back chains)."""
+    """Genome lengths around the tiles (8,192 slots for u64 keys, 16,384 for u32;
+    the lengths around round 4's 4,096 / 8,192 tiles stay in the list) and 300
+    small genomes in one batch (many tiles, many look-back chains)."""
     rng = np.random.default_rng(9)
     blobs = []
     for L in [1, 2046, 2047, 2048, 2049, 4095, 4096, 4097, 6143, 6145, 8191, 8192, 8193, 12289, 16383, 16385]:

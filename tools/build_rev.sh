@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build the HIP library of git revision REV into OUT (for process-level A/B runs
-# against the working tree: KF2VEC_GPU_LIB=OUT python tools/ab_bench.py ...).
+# against the working tree: KF2VEC_ALLOW_FOREIGN_LIB=1 KF2VEC_GPU_LIB=OUT python tools/...;
+# _native refuses a library built from other sources unless that is set).
 #   tools/build_rev.sh HEAD~1 kf2vecfsw_amd/libkf2vec_gpu_prev.so
 set -eu
 REV=$1; OUT=$2
