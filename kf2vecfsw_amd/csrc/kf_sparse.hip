@@ -5,31 +5,41 @@
 // and keeps the PRESENT canonical k-mers only (main.py:133-160); its parser
 // accepts k = 2..31 (main.py:81-82, 1006).  A dense 4^k/2-bin row stops being
 // possible past k ~ 13 (k = 31: 2^61 bins), so this path sorts instead of
-// histogramming:
-//   1. emit    one key per input byte: the canonical code of the window ending
-//              at that byte (standard 2-bit code A0 C1 G2 T3, canonical = the
-//              smaller of the code and its reverse complement, i.e. the
-//              lexicographically smaller string), or SENT (= 4^k - 1, the code of
-//              T..T, never canonical) where no window ends;
-//   2. sort    each genome's keys, a segmented LSD radix sort of 2k bits in
-//              ceil(2k/8) passes of equal <= 8-bit digits: one read counts every
-//              pass's digits per genome, then each pass is one single-sweep
-//              kernel (ranks by LDS atomics, the tile's digit offsets by
-//              decoupled look-back over the genome's earlier tiles, the tile
-//              re-ordered in LDS so every digit's keys leave as one run);
-//   3. unique  run heads of the sorted keys compacted with their positions; a
-//              run's count is the distance to the next head.  SENT sorts last and
-//              is dropped.
-// Keys are u32 for k <= 16 (half the bytes of every pass) and u64 above.
+// histogramming.  Round 5: one most-significant-digit split in HBM, then the
+// sort of each bucket group inside one CU's LDS (rounds 4's form was an LSD
+// radix sort of 2k bits with one HBM read + write of every key per 8-bit digit,
+// 8 passes at k = 31):
+//   A. count    every window's canonical key (standard 2-bit code A0 C1 G2 T3,
+//               canonical = the smaller of the code and its reverse complement,
+//               i.e. the lexicographically smaller string) is computed from the
+//               input bytes and counted by its top D <= 10 bits (its bucket) per
+//               genome; nothing is written but the genome x bucket totals;
+//   B. scatter  the keys are computed again (the input is 1 B per key, a key 4-8 B)
+//               and written bucket by bucket: per tile of 16,384 bytes, ranks by
+//               LDS atomics, each bucket's place among the genome's earlier tiles
+//               by decoupled look-back, the tile re-ordered in LDS so every
+//               bucket's keys leave as one run;
+//   C. chunks   consecutive buckets of a genome are grouped into chunks of at most
+//               C keys (128 KiB of LDS); one workgroup loads a chunk, sorts it in
+//               LDS (LSD passes of 8 bits over the bits below the chunk's first
+//               bucket), run-length encodes it, learns how many distinct k-mers
+//               the genome's earlier chunks hold (look-back) and writes its
+//               (key, count) pairs in place.  A bucket with more than C keys
+//               (low-complexity sequence: poly-A puts a genome's every window in
+//               one bucket) is copied to an overflow area, sorted there by the
+//               round-4 LSD passes (single sweep, look-back) and run-length
+//               encoded by one workgroup streaming it.
+// Keys are u32 for k <= 16 and u64 above.  Windows that end nowhere (no base,
+// a break) produce no key (round 4 sorted a sentinel per byte).
 //
 // Semantics are those of the dense counter (kf_count_batch): '\n' is
 // transparent, any other non-ACGT byte (either case counts) breaks the window,
 // the excluded byte ranges (headers, FASTQ '+' / quality lines, from
 // kf_index_records) break it too, and a window never spans two genomes.
 //
-// Layout: genome g owns key slots [goff[g], goff[g+1]) in every buffer (a genome
-// has at most as many windows as bytes), cut into tiles (TileOf); tile t of
-// the batch belongs to the genome g with tfirst[g] <= t < tfirst[g+1].
+// Layout: genome g owns slots [goff[g], goff[g+1]) of every key buffer (a genome
+// has at most as many windows as bytes); its bucketed keys fill the first
+// gkeys[g] of them, bucket b from gbase[g][b].
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,29 +48,42 @@
 namespace kf {
 namespace {
 
-constexpr int kSBlock = 256;                   // threads per workgroup (4 waves)
+constexpr int kSBlock = 256;                   // LSD (overflow) kernels: threads per workgroup
 constexpr int kSWaves = kSBlock / 64;
 constexpr int kEB = 32;                        // emit: bytes per thread
-// Key slots per tile: 16384 u32 keys or 8192 u64 keys (64 / 32 keys per 8-bit
-// digit run on average, 256-byte runs; the scatter stages 64 KiB).  With the
-// single-sweep passes fewer, larger tiles win despite 2-3 waves per SIMD
-// (profiles/r04/v49_*, v51_*: k = 31 17.1 -> 15.2 ms against u64 4096, k = 16
-// 7.14 -> 6.81 against u32 8192).
+// LSD tiles (the overflow sort): 16384 u32 keys or 8192 u64 keys (the scatter
+// stages 64 KiB; profiles/r04/v49_*, v51_*).
 template <typename KeyT>
 struct TileOf {
-#ifndef KF_SPARSE_TILE64   // u64 tile (tools/ A/B builds)
-#define KF_SPARSE_TILE64 8192
-#endif
-#ifndef KF_SPARSE_TILE32   // u32 tile (tools/ A/B builds)
-#define KF_SPARSE_TILE32 16384
-#endif
-    static constexpr uint32_t tile = sizeof(KeyT) == 4 ? (uint32_t)KF_SPARSE_TILE32 : (uint32_t)KF_SPARSE_TILE64;
+    static constexpr uint32_t tile = sizeof(KeyT) == 4 ? 16384u : 8192u;
     static constexpr int per = tile / kSBlock;             // slots per thread
     static constexpr uint32_t wave_span = tile / kSWaves;  // slots per wave
-    static constexpr int emit_threads = tile / kEB;        // emit: kEB bytes per thread
-    static_assert(emit_threads % 64 == 0 && emit_threads <= 1024, "emit: whole waves per tile");
 };
-constexpr uint32_t tile_for_k(int k) { return k <= 16 ? TileOf<uint32_t>::tile : TileOf<uint64_t>::tile; }
+
+// Phase A / B tiles: 16,384 input bytes, 512 threads x kEB bytes.
+constexpr uint32_t kTB = 16384;
+constexpr int kBBlock = (int)kTB / kEB;        // 512
+constexpr int kBWaves = kBBlock / 64;          // 8
+// Buckets: the top D bits of a 2k-bit key, D = min(10, 2k).
+constexpr int kBD = 10;
+constexpr uint32_t kNB = 1u << kBD;
+__host__ __device__ constexpr int sp_dbits(int k) { return 2 * k < kBD ? 2 * k : kBD; }
+// Phase C: chunks of at most C keys (128 KiB of LDS), 1024 threads.
+constexpr int kCBlock = 512;   // 8 waves: 32 keys per thread, up to 256 VGPRs (1024 threads spilled at 128)
+constexpr int kCWaves = kCBlock / 64;
+template <typename KeyT>
+struct ChunkOf {
+    static constexpr uint32_t cap = 16384;                          // keys (128 KiB of u64, 64 KiB of u32)
+    static constexpr int per = cap / kCBlock;                       // keys per thread
+    static constexpr uint32_t wave_span = cap / kCWaves;
+};
+constexpr uint32_t kNoOvf = 0xFFFFFFFFu;
+struct Chunk {          // one LDS sort unit: buckets [blo, blo + nb) of one genome
+    uint32_t start;     // first slot in the bucketed keys
+    uint32_t nkeys;
+    uint16_t blo, nb;
+    uint32_t ovf;       // kNoOvf, or the big bucket's first slot in the overflow area
+};
 
 // Standard 2-bit code of a byte: A0 C1 G2 T3 (either case), 4 = '\n', 5 = other.
 // Branch-free (a switch compiled to a compare tree with exec-mask branches per
@@ -74,8 +97,8 @@ __device__ __forceinline__ uint32_t sp_code(uint8_t c) {
     return base ? (x ^ (x >> 1)) : (c == '\n' ? 4u : 5u);
 }
 
-// Genome of tile t (t < tfirst[n]): the last g with tfirst[g] <= t (empty
-// genomes share their tfirst with the next genome).
+// Segment of tile t (t < tfirst[n]): the last g with tfirst[g] <= t (empty
+// segments share their tfirst with the next one).
 __device__ __forceinline__ int tile_genome(const uint32_t* tfirst, int n, uint32_t t) {
     int lo = 0, hi = n;
     while (hi - lo > 1) {
@@ -87,10 +110,10 @@ __device__ __forceinline__ int tile_genome(const uint32_t* tfirst, int n, uint32
 }
 
 struct TileSpan {
-    uint32_t g, gs, ge, base, cnt;   // genome, its slot range, the tile's first slot and slot count
+    uint32_t g, gs, ge, base, cnt;   // segment, its slot range, the tile's first slot and slot count
 };
 
-// tfirst[n + 2 + t] = the genome of tile t (sp_tilemap_kernel): one load
+// tfirst[n + 2 + t] = the segment of tile t (sp_tilemap_kernel): one load
 // instead of a binary search's chain of dependent loads at every tile's start
 __device__ __forceinline__ bool tile_span(const uint64_t* goff, const uint32_t* tfirst, int n, uint32_t t,
                                           TileSpan& ts, uint32_t span) {
@@ -103,8 +126,10 @@ __device__ __forceinline__ bool tile_span(const uint64_t* goff, const uint32_t* 
     return true;
 }
 
-// Exclusive prefix of one value per thread over the 256-thread workgroup.
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum) {
+// Exclusive prefix of one value per thread over an NW-wave workgroup; *total
+// (optional) gets the sum.  Contains two barriers.
+template <int NW>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total = nullptr) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t inc = v;
     for (int d = 1; d < 64; d <<= 1) {
@@ -113,38 +138,17 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum) 
     }
     if (lane == 63) wsum[w] = inc;
     __syncthreads();
-    uint32_t before = 0;
-    for (int x = 0; x < w; ++x) before += wsum[x];
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) {
+        const uint32_t s = wsum[x];
+        before += x < w ? s : 0u;
+        all += s;
+    }
+    if (total) *total = all;
     __syncthreads();
     return before + inc - v;
 }
-
-// Ranking inside a wave-instruction of the stable scatter:
-//   1 (default): LDS atomics, one returning add per key into the wave's digit
-//     counter -- an LDS unit serves the lanes of one instruction that hit the
-//     same address in lane order, so ranks follow the keys' order;
-//   0: ballot matching (one ballot per digit bit; ~46 VALU per 64 keys), which
-//     needs no such ordering.
-// The heads kernel checks every genome's final order (a key below its
-// predecessor flags the call: all counts come back UINT64_MAX - 1), so an
-// ordering the hardware did not keep cannot pass silently.
-#ifndef KF_SPARSE_RANK
-#define KF_SPARSE_RANK 1
-#endif
-
-#if KF_SPARSE_RANK == 0
-// Lanes of the wave (among `valid`) whose digit equals this lane's: one ballot
-// per digit bit.
-__device__ __forceinline__ uint64_t match_digit(uint32_t d, int bits, uint64_t valid) {
-    uint64_t m = valid;
-    for (int b = 0; b < bits; ++b) {
-        const bool one = (d >> b) & 1u;
-        const uint64_t bb = __ballot(one);
-        m &= one ? bb : ~bb;
-    }
-    return m;
-}
-#endif
 
 // ---- tiles: tfirst[g] = exclusive prefix of ceil(len_g / span), tfirst[n] = total.
 // A goff that decreases or ends past batch_bytes (the buffers' size) sets
@@ -183,7 +187,7 @@ __global__ void __launch_bounds__(1024) sp_tiles_kernel(const uint64_t* goff, in
     }
 }
 
-// ---- tile map: tfirst[n + 2 + t] = genome of tile t; xlo[t] = the first
+// ---- tile map: tfirst[n + 2 + t] = segment of tile t; xlo[t] = the first
 // excluded range ending after the tile's first slot (xlo[tiles] = n_excl)
 __global__ void __launch_bounds__(256) sp_tilemap_kernel(const uint64_t* goff, uint32_t* tfirst, int n,
                                                          const uint64_t* excl, uint32_t n_excl, uint32_t span,
@@ -206,30 +210,17 @@ __global__ void __launch_bounds__(256) sp_tilemap_kernel(const uint64_t* goff, u
     xlo[t] = lo;
 }
 
-// ---- 1. emit: thread = kEB consecutive bytes of a tile; its k-1 bases
-// of context come from a walk back over the bytes before it (newlines skipped; a
-// break, an excluded range or the genome start ends the walk), then it rolls
-// forward.  32 bytes per thread amortise the walk (up to k-1 + newline bytes).
-
-// The keys go out through LDS: a thread's kEB keys are one row (padded by 16 bytes
-// against bank conflicts), read back key by key in lane order so that every store
-// instruction writes 256-512 contiguous bytes (a thread storing its own 128-256
-// bytes touches 64 lines per instruction).
-#ifndef KF_SPARSE_EMIT   // 1: whole rows staged, 2: half rows (half the LDS), 0: direct stores
-#define KF_SPARSE_EMIT 2
-#endif
+// ---- keys of the windows ending in kEB bytes: thread = kEB consecutive bytes
+// of tile tix (span kTB); its k-1 bases of context come from a walk back over
+// the bytes before it (newlines skipped; a break, an excluded range or the
+// genome start ends the walk), then it rolls forward.  32 bytes per thread
+// amortise the walk (up to k-1 + newline bytes).  out[] holds SENT on entry
+// (4^k - 1 = T..T, never canonical: its reverse complement A..A is smaller) and
+// keeps it where no window ends.
 template <typename KeyT>
-struct EmitStage {
-    static constexpr int keys = KF_SPARSE_EMIT == 2 ? kEB / 2 : kEB;   // keys per row per round
-    static constexpr int row = keys + 16 / (int)sizeof(KeyT);          // padded row
-    static constexpr int elems = KF_SPARSE_EMIT == 0 ? 1 : TileOf<KeyT>::emit_threads * row;
-};
-
-// One thread's keys (out[] holds SENT on entry): the windows ending in the kEB
-// bytes at p0 = ts.base + threadIdx.x * kEB.
-template <typename KeyT>
-__device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, const TileSpan& ts, uint32_t n_excl,
-                                         const uint64_t* excl, const uint32_t* xlo, int k, KeyT (&out)[kEB]) {
+__device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, const TileSpan& ts, uint32_t tix,
+                                         uint32_t n_excl, const uint64_t* excl, const uint32_t* xlo, int k,
+                                         KeyT (&out)[kEB]) {
     const uint32_t q0 = threadIdx.x * kEB;
     if (q0 >= ts.cnt) return;
     const uint32_t p0 = ts.base + q0, cnt = min((uint32_t)kEB, ts.cnt - q0);
@@ -254,11 +245,10 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
         }
     }
     if (!any) return;   // no base here: no window ends in these bytes (and no walk back over a newline run)
-    // first excluded range ending after p0
+    // first excluded range ending after p0: in [xlo[tix], xlo[tix + 1]] (sp_tilemap_kernel)
     uint32_t ix = 0;
     {
-        // the answer lies in [xlo[t], xlo[t + 1]] (sp_tilemap_kernel)
-        uint32_t lo = xlo[blockIdx.x], h = xlo[blockIdx.x + 1];
+        uint32_t lo = xlo[tix], h = xlo[tix + 1];
         while (lo < h) {
             const uint32_t m = (lo + h) >> 1;
             if (excl[2 * m + 1] <= p0) lo = m + 1;
@@ -329,246 +319,121 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
     }
 }
 
-template <typename KeyT>
-__global__ void __launch_bounds__(TileOf<KeyT>::emit_threads) sp_emit_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
-                                                            const uint32_t* tfirst, int n, const uint64_t* excl,
-                                                            uint32_t n_excl, const uint32_t* xlo, int k,
-                                                            KeyT* __restrict__ keys) {
-    using T = TileOf<KeyT>;
-    using S = EmitStage<KeyT>;
-    __shared__ __attribute__((aligned(16))) KeyT stage[S::elems];
-    TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;   // uniform over the workgroup
-    const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
-    KeyT out[kEB];
-#pragma unroll
-    for (int j = 0; j < kEB; ++j) out[j] = sent;
-    emit_row(bytes, ts, n_excl, excl, xlo, k, out);
-#if KF_SPARSE_EMIT == 0
-    (void)stage;
-    const uint32_t q0 = threadIdx.x * kEB;
-    if (q0 < ts.cnt) {
-        KeyT* dst = keys + ts.base + q0;
-        const uint32_t cnt = min((uint32_t)kEB, ts.cnt - q0);
-        if (cnt == (uint32_t)kEB && ((uintptr_t)dst & 15u) == 0) {
-#pragma unroll
-            for (int j = 0; j < kEB; j += 16 / (int)sizeof(KeyT)) {
-                if constexpr (sizeof(KeyT) == 8) *(ulonglong2*)(dst + j) = make_ulonglong2(out[j], out[j + 1]);
-                else *(uint4*)(dst + j) = make_uint4(out[j], out[j + 1], out[j + 2], out[j + 3]);
-            }
-        } else {
-            for (uint32_t j = 0; j < cnt; ++j) dst[j] = out[j];
-        }
-    }
-#else
-    KeyT* row = stage + threadIdx.x * S::row;
-    KeyT* dst = keys + ts.base;
-#pragma unroll
-    for (int h = 0; h < kEB / S::keys; ++h) {
-        if (h) __syncthreads();   // the previous round's reads are done
-#pragma unroll
-        for (int j = 0; j < S::keys; j += 16 / (int)sizeof(KeyT)) {
-            const int o = h * S::keys + j;
-            if constexpr (sizeof(KeyT) == 8) *(ulonglong2*)(row + j) = make_ulonglong2(out[o], out[o + 1]);
-            else *(uint4*)(row + j) = make_uint4(out[o], out[o + 1], out[o + 2], out[o + 3]);
-        }
-        __syncthreads();
-        // staged key e = (thread r, key c) is slot r * kEB + h * S::keys + c of the tile
-#pragma unroll 4
-        for (uint32_t e = threadIdx.x; e < (uint32_t)T::emit_threads * S::keys; e += T::emit_threads) {
-            const uint32_t r = e / S::keys, c = e % S::keys, i = r * kEB + h * S::keys + c;
-            if (i < ts.cnt) dst[i] = stage[r * S::row + c];
-        }
-    }
-#endif
-}
-
-// ---- 2a. per-tile digit histogram (one row per digit: hist[d * hstride + t])
-template <typename KeyT>
-__global__ void __launch_bounds__(kSBlock) sp_hist_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
-                                                          const uint32_t* tfirst, int n, int shift, int bits,
-                                                          uint32_t* hist, uint32_t hstride) {
-    using T = TileOf<KeyT>;
-    __shared__ uint32_t wc[kSWaves][256];
-    TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int i = tid; i < kSWaves * 256; i += kSBlock) (&wc[0][0])[i] = 0;
-    __syncthreads();
-    const uint32_t dmask = (1u << bits) - 1u;
-    // order does not matter here: one LDS add per key into the wave's counters
-    // (the ballot matching of the scatter costs ~60 VALU per 64 keys)
-    // every load first (a load per iteration, each waited for before its add,
-    // left the waves at HBM latency): indices clamped to the tile's last key
-    KeyT x[T::per];
-#pragma unroll
-    for (int it = 0; it < T::per; ++it) x[it] = keys[ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1)];
-#pragma unroll
-    for (int it = 0; it < T::per; ++it) {
-        const uint32_t li = w * T::wave_span + it * 64 + lane;
-        if (li < ts.cnt) atomicAdd(&wc[w][(uint32_t)(x[it] >> shift) & dmask], 1u);
-    }
-    __syncthreads();
-    if (tid <= (int)dmask) hist[(uint64_t)tid * hstride + blockIdx.x] = wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
-}
-
-// ---- 2b. workgroup (g, d): exclusive scan of hist[d][tiles of g] in place;
-// gtot[g * 256 + d] = the genome's count of digit d
-__global__ void __launch_bounds__(kSBlock) sp_scan_kernel(uint32_t* hist, uint32_t hstride, const uint32_t* tfirst,
-                                                          uint32_t* gtot) {
-    __shared__ uint32_t wsum[kSWaves];
-    __shared__ uint32_t tot;
-    const uint32_t g = blockIdx.x, d = blockIdx.y;
-    uint32_t* row = hist + (uint64_t)d * hstride;
-    const uint32_t t0 = tfirst[g], t1 = tfirst[g + 1];
-    uint32_t carry = 0;
-    for (uint32_t base = t0; base < t1; base += kSBlock) {
-        const uint32_t t = base + threadIdx.x;
-        const uint32_t v = t < t1 ? row[t] : 0u;
-        const uint32_t ex = block_excl_scan(v, wsum);
-        if (t < t1) row[t] = carry + ex;
-        if (threadIdx.x == kSBlock - 1) tot = ex + v;   // the chunk's total
-        __syncthreads();
-        carry += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) gtot[g * 256 + d] = carry;
-}
-
-// ---- 2c. stable scatter of one tile by digit
-// ---- 2'. single-sweep passes (KF_SPARSE_LOOKBACK = 1, the default): no tile
-// histogram pass and no scan.  The genome-wide digit counts of EVERY pass come
-// from one read of the emitted keys (sp_ghist_kernel); inside a pass, tile t
-// learns how many keys of digit d its genome's earlier tiles hold by decoupled
-// look-back: it publishes its own count (AGG), adds up its predecessors' words
-// back to the first inclusive prefix (INCL), then publishes its own INCL.  A
-// status word is (epoch << 34 | flag << 32 | count), one 64-bit store, so count
-// and flag are seen together; epoch = pass + 1 tells this pass's words from the
-// last pass's (the array is cleared once per call).  Tiles are numbered in the
-// order workgroups start (a ticket), so a tile only waits on tiles that are
-// already running; a wait that still exceeds ~2^22 polls flags the call (bit 2
-// of tfirst[n+1]: every count comes back UINT64_MAX - 1) instead of hanging.
-#ifndef KF_SPARSE_LOOKBACK
-#define KF_SPARSE_LOOKBACK 1
-#endif
-#ifndef KF_SPARSE_ABL   // profiling ablations of the scatter (tools/ builds; wrong order by design)
-#define KF_SPARSE_ABL 0
-#endif
-#ifndef KF_SPARSE_LBW   // predecessors read per look-back round trip
-#define KF_SPARSE_LBW 1   // 4 and 8 measured the same with the interleaved order (v39)
-#endif
+// ---- decoupled look-back (phase B per bucket, phase C per chunk, the LSD
+// passes per digit).  A status word is (epoch << 34 | flag << 32 | count), one
+// 64-bit store, so count and flag are seen together; epoch tells this pass's
+// words from an earlier pass's (the arrays are cleared once per call).  Units
+// are taken in ticket order, so a unit only waits on units already running; a
+// wait that still exceeds ~2^22 polls sets bit 1 of *flags (every count then
+// comes back UINT64_MAX - 1) instead of hanging.
 constexpr uint64_t kStAgg = 1, kStIncl = 2;
 
 __device__ __forceinline__ void st_publish(uint64_t* w, uint32_t epoch, uint64_t flag, uint32_t v) {
     __hip_atomic_store(w, ((uint64_t)epoch << 34) | (flag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ uint32_t lookback(uint64_t* status, uint32_t* tfirst, int n, uint32_t t, uint32_t t0,
-                                             uint32_t d, uint32_t tot, uint32_t epoch) {
-    uint64_t* mine = status + (uint64_t)t * 256 + d;
-    if (t == t0) {   // the genome's first tile: its prefix is its count
+// Unit t's exclusive prefix of one counter (unit u's word at status[u * stride]),
+// its chain starting at unit t0; publishes t's inclusive prefix.
+__device__ __forceinline__ uint32_t lookback(uint64_t* status, uint32_t stride, uint32_t* flags, uint32_t t,
+                                             uint32_t t0, uint32_t tot, uint32_t epoch) {
+    uint64_t* mine = status + (uint64_t)t * stride;
+    if (t == t0) {   // the chain's first unit: its prefix is its count
         st_publish(mine, epoch, kStIncl, tot);
         return 0;
     }
     st_publish(mine, epoch, kStAgg, tot);
-    // KF_SPARSE_LBW predecessors per round trip (a status load goes past the
-    // XCD's L2: ~1-2 us), nearest first, summed up to the first inclusive word;
-    // a word not yet published ends the round there and is polled again
-    uint32_t before = 0;
-    uint32_t spins = 0;
+    uint32_t before = 0, spins = 0;
     uint32_t j = t - 1;   // nearest predecessor not yet added (>= t0)
     for (;;) {
-        uint64_t w[KF_SPARSE_LBW];
-#pragma unroll
-        for (int q = 0; q < KF_SPARSE_LBW; ++q)
-            w[q] = __hip_atomic_load(status + (uint64_t)(j >= t0 + (uint32_t)q ? j - (uint32_t)q : t0) * 256 + d, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-        bool done = false, stalled = false;
-#pragma unroll
-        for (int q = 0; q < KF_SPARSE_LBW; ++q) {
-            if (done || stalled) continue;
-            if ((uint32_t)(w[q] >> 34) != epoch) {   // not published yet
-                stalled = true;
-                continue;
-            }
-            before += (uint32_t)w[q];
-            if (((w[q] >> 32) & 3u) == kStIncl || j == t0) done = true;
-            else --j;
-        }
-        if (done) break;
-        if (stalled) {
+        const uint64_t w = __hip_atomic_load(status + (uint64_t)j * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(w >> 34) != epoch) {   // not published yet
             if (++spins > (1u << 22)) {
-                atomicOr(&tfirst[n + 1], 2u);
+                atomicOr(flags, 2u);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
+            continue;
         }
+        before += (uint32_t)w;
+        if (((w >> 32) & 3u) == kStIncl || j == t0) break;
+        --j;
     }
     st_publish(mine, epoch, kStIncl, before + tot);
     return before;
 }
 
-// gall[(p * n + g) * 256 + d] += keys of genome g with digit d in pass p.
-// Workgroup (g, c) takes the c-th of gridDim.y slices of genome g.
+// ---- LSD passes (the overflow sort of big buckets; round 4's sort of whole genomes)
+// gall[(p * n + g) * 256 + d] += keys of segment g with digit d in pass p.
+// Workgroups loop over the segments (most are empty when nothing overflows).
 template <typename KeyT>
 __global__ void __launch_bounds__(kSBlock) sp_ghist_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
                                                            const uint32_t* tfirst, int n, int passes, int bits,
                                                            uint32_t* gall) {
     __shared__ uint32_t cnt[8][256];
     if (tfirst[n + 1] & 1u) return;   // invalid goff (sp_tiles_kernel): nothing is counted
-    const int g = blockIdx.x;
-    const uint32_t gs = (uint32_t)goff[g], len = (uint32_t)goff[g + 1] - gs;
-    const uint32_t part = (len + gridDim.y - 1) / gridDim.y;
-    const uint32_t c0 = gs + min(len, blockIdx.y * part), c1 = gs + min(len, (blockIdx.y + 1) * part);
-    if (c0 >= c1) return;
-    for (int i = threadIdx.x; i < passes * 256; i += kSBlock) (&cnt[0][0])[i] = 0;
-    __syncthreads();
-    const uint32_t dmask = (1u << bits) - 1u;   // digits above bit 2k are 0
-    constexpr int kB = 8;
-    for (uint32_t base = c0; base < c1; base += kSBlock * kB) {
-        KeyT x[kB];
+    const uint32_t dmask = (1u << bits) - 1u;
+    for (int g = blockIdx.x; g < n; g += gridDim.x) {
+        const uint32_t c0 = (uint32_t)goff[g], c1 = (uint32_t)goff[g + 1];
+        if (c0 >= c1) continue;   // uniform
+        for (int i = threadIdx.x; i < passes * 256; i += kSBlock) (&cnt[0][0])[i] = 0;
+        __syncthreads();
+        constexpr int kB = 8;
+        for (uint32_t base = c0; base < c1; base += kSBlock * kB) {
+            KeyT x[kB];
 #pragma unroll
-        for (int j = 0; j < kB; ++j) x[j] = keys[min(base + j * kSBlock + threadIdx.x, c1 - 1)];
+            for (int j = 0; j < kB; ++j) x[j] = keys[min(base + j * kSBlock + threadIdx.x, c1 - 1)];
 #pragma unroll
-        for (int j = 0; j < kB; ++j) {
-            if (base + j * kSBlock + threadIdx.x < c1) {
-                for (int p = 0; p < passes; ++p) atomicAdd(&cnt[p][(uint32_t)(x[j] >> (p * bits)) & dmask], 1u);
+            for (int j = 0; j < kB; ++j) {
+                if (base + j * kSBlock + threadIdx.x < c1) {
+                    for (int p = 0; p < passes; ++p) atomicAdd(&cnt[p][(uint32_t)(x[j] >> (p * bits)) & dmask], 1u);
+                }
             }
         }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < passes * 256; i += kSBlock) {
-        const uint32_t v = (&cnt[0][0])[i];
-        if (v) atomicAdd(&gall[((uint64_t)(i >> 8) * n + g) * 256 + (i & 255)], v);
+        __syncthreads();
+        for (int i = threadIdx.x; i < passes * 256; i += kSBlock) {
+            const uint32_t v = (&cnt[0][0])[i];
+            if (v) atomicAdd(&gall[((uint64_t)(i >> 8) * n + g) * 256 + (i & 255)], v);
+        }
+        __syncthreads();
     }
 }
 
-// Ticket -> tile for the single-sweep passes: tiles ordered by (index inside
-// the genome, genome), so the tiles running at once spread over the genomes'
-// independent look-back chains instead of queueing on one genome's chain.
-// Inside a genome the order is kept (what the look-back's progress needs).
-// O(n) per tile: used up to KF_SPARSE_ORDER_MAXN genomes (identity above).
+// Ticket -> unit (tiles of the passes, tiles of phase B, chunks of phase C):
+// units ordered by (index inside the segment, segment), so the units running at
+// once spread over the segments' independent look-back chains instead of
+// queueing on one chain.  Inside a segment the order is kept (what the
+// look-back's progress needs).  O(n) per unit: used up to KF_SPARSE_ORDER_MAXN
+// segments (identity above).  ufirst: prefix of units per segment, the total at
+// [n], the unit -> segment map from [n + 2].
 #ifndef KF_SPARSE_ORDER_MAXN
 #define KF_SPARSE_ORDER_MAXN 4096
 #endif
-__global__ void __launch_bounds__(kSBlock) sp_order_kernel(const uint32_t* tfirst, int n, uint32_t* order) {
+__global__ void __launch_bounds__(kSBlock) sp_order_kernel(const uint32_t* ufirst, int n, uint32_t* order) {
     const uint32_t t = blockIdx.x * kSBlock + threadIdx.x;
-    if (t >= tfirst[n]) return;
-    const int g = (int)tfirst[n + 2 + t];
-    const uint32_t r = t - tfirst[g];
+    if (t >= ufirst[n]) return;
+    const int g = (int)ufirst[n + 2 + t];
+    const uint32_t r = t - ufirst[g];
     uint32_t pos = 0;
     for (int h = 0; h < n; ++h) {
-        const uint32_t nt = tfirst[h + 1] - tfirst[h];
+        const uint32_t nt = ufirst[h + 1] - ufirst[h];
         pos += min(nt, r) + (h < g && nt > r ? 1u : 0u);
     }
     order[pos] = t;
 }
 
-template <typename KeyT, bool LB>
+// One single-sweep LSD pass (stable scatter by one digit): a tile loads its keys,
+// ranks them with one returning LDS add per key into its wave's digit counter,
+// learns how many keys of each digit its segment's earlier tiles hold by
+// look-back, re-orders the tile in LDS by digit and writes every digit's keys as
+// one run.  Persistent: the workgroups loop over tickets (an empty overflow area
+// costs one ticket per workgroup).  The ranks rely on an LDS unit serving the
+// lanes of one instruction that hit the same address in lane order (ranks then
+// follow the keys' order); the run-length encoding checks the final order and
+// flags the call if it is broken.
+template <typename KeyT>
 __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restrict__ in, KeyT* __restrict__ out,
                                                              const uint64_t* goff, uint32_t* tfirst, int n,
-                                                             int shift, int bits, const uint32_t* hist,
-                                                             uint32_t hstride, const uint32_t* gtot,
+                                                             int shift, int bits, const uint32_t* gtot,
                                                              uint64_t* status, uint32_t* ticket, uint32_t epoch,
                                                              const uint32_t* order) {
     using T = TileOf<KeyT>;
@@ -578,255 +443,556 @@ __global__ void __launch_bounds__(kSBlock) sp_scatter_kernel(const KeyT* __restr
     __shared__ uint32_t wsum[kSWaves];
     __shared__ uint32_t tix;
     extern __shared__ __attribute__((aligned(16))) uint8_t sp_dyn[];
-    KeyT* stage = (KeyT*)sp_dyn;   // T::tile keys (dynamic LDS: 32 KiB)
-    uint32_t t = blockIdx.x;
-    if constexpr (LB) {   // tiles in the order workgroups start: a tile only waits on started tiles
-        if (threadIdx.x == 0) {
+    KeyT* stage = (KeyT*)sp_dyn;   // T::tile keys (dynamic LDS: 64 KiB)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t dmask = (1u << bits) - 1u;
+    for (;;) {
+        if (tid == 0) {
             const uint32_t x = atomicAdd(ticket, 1u);
             tix = order && x < tfirst[n] ? order[x] : x;
         }
         __syncthreads();
-        t = tix;
-    }
-    TileSpan ts;
-    if (!tile_span(goff, tfirst, n, t, ts, T::tile)) return;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int i = tid; i < kSWaves * 256; i += kSBlock) (&wc[0][0])[i] = 0;
-    __syncthreads();
-    const uint32_t dmask = (1u << bits) - 1u;
-    const uint64_t lt = (1ull << lane) - 1;
-    KeyT key[T::per];
-    uint32_t rank[T::per];
+        const uint32_t t = tix;
+        TileSpan ts;
+        if (!tile_span(goff, tfirst, n, t, ts, T::tile)) return;   // uniform: no tiles left
+        for (int i = tid; i < kSWaves * 256; i += kSBlock) (&wc[0][0])[i] = 0;
+        __syncthreads();
+        KeyT key[T::per];
+        uint32_t rank[T::per];
 #pragma unroll
-    for (int it = 0; it < T::per; ++it) key[it] = in[ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1)];
-#pragma unroll
-    for (int it = 0; it < T::per; ++it) {
-        const uint32_t li = w * T::wave_span + it * 64 + lane;
-        const bool v = li < ts.cnt;
-        const KeyT x = key[it];
-        const uint32_t d = (uint32_t)(x >> shift) & dmask;
-#if KF_SPARSE_RANK == 0
-        const uint64_t m = match_digit(d, bits, __ballot(v));
-        const uint32_t r = (uint32_t)__popcll(m & lt);
-        const uint32_t prior = wc[w][d];
-        if (v && r == 0) wc[w][d] = prior + (uint32_t)__popcll(m);
-        rank[it] = prior + r;
-#else
-        (void)lt;
-#if KF_SPARSE_ABL == 3   // profiling only: no rank atomics
-        rank[it] = 0u;
-        if (v && lane == 0) wc[w][d] += 64u;
-#else
-        rank[it] = v ? atomicAdd(&wc[w][d], 1u) : 0u;
-#endif
-#endif
-    }
-    __syncthreads();
-    {
-        const int d = tid;   // one digit per thread (bits <= 8)
-        const uint32_t c0 = wc[0][d], c1 = wc[1][d], c2 = wc[2][d], c3 = wc[3][d];
-        const bool live = d <= (int)dmask;
-        const uint32_t tot = c0 + c1 + c2 + c3;
-        const uint32_t gt = live ? gtot[ts.g * 256 + d] : 0u;
-        uint32_t before;   // keys of digit d in the genome's earlier tiles
-        if constexpr (LB) {
-#if KF_SPARSE_ABL == 1   // profiling only (wrong order): no look-back
-            before = 0u;
-            (void)status;
-            (void)epoch;
-#else
-            before = live ? lookback(status, tfirst, n, t, tfirst[ts.g], d, tot, epoch) : 0u;
-#endif
-        } else {
-            before = live ? hist[(uint64_t)d * hstride + t] : 0u;
-        }
-        const uint32_t lb = block_excl_scan(tot, wsum);
-        const uint32_t gb = block_excl_scan(gt, wsum);
-        wc[0][d] = 0;
-        wc[1][d] = c0;
-        wc[2][d] = c0 + c1;
-        wc[3][d] = c0 + c1 + c2;
-        lbase[d] = lb;
-        gdst[d] = live ? ts.gs + gb + before - lb : 0u;
-    }
-    __syncthreads();
-    for (int it = 0; it < T::per; ++it) {
-        const uint32_t li = w * T::wave_span + it * 64 + lane;
-        if (li < ts.cnt) {
-            const uint32_t d = (uint32_t)(key[it] >> shift) & dmask;
-            stage[lbase[d] + wc[w][d] + rank[it]] = key[it];
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < ts.cnt; i += kSBlock) {
-        const KeyT x = stage[i];
-#if KF_SPARSE_ABL == 2   // profiling only: no global stores (one per tile)
-        if (i == 0)
-#endif
-        out[gdst[(uint32_t)(x >> shift) & dmask] + i] = x;
-    }
-}
-
-// The key before slot li of the wave-span layout (li = w * wave_span + it * 64 +
-// lane): lane - 1 of the same load, lane 63 of the previous one, or for the
-// wave's first slot one extra (wave-uniform) load -- one key load per slot
-// instead of two.
-template <typename KeyT>
-__device__ __forceinline__ KeyT wave_shfl(KeyT v, int src, bool up) {
-    if constexpr (sizeof(KeyT) == 8) {
-        const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-        const uint32_t l = (uint32_t)(up ? __shfl_up((int)lo, 1, 64) : __shfl((int)lo, src, 64));
-        const uint32_t h = (uint32_t)(up ? __shfl_up((int)hi, 1, 64) : __shfl((int)hi, src, 64));
-        return ((KeyT)h << 32) | l;
-    } else {
-        return (KeyT)(up ? __shfl_up((int)v, 1, 64) : __shfl((int)v, src, 64));
-    }
-}
-
-// every key of the lane first; returns the key before the wave's first slot
-template <typename KeyT>
-__device__ __forceinline__ KeyT load_keys(const KeyT* __restrict__ keys, const TileSpan& ts, int w, int lane,
-                                          KeyT (&x)[TileOf<KeyT>::per]) {
-    using T = TileOf<KeyT>;
-#pragma unroll
-    for (int it = 0; it < T::per; ++it) x[it] = keys[ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1)];
-    const uint32_t p0 = ts.base + min(w * T::wave_span, ts.cnt - 1);
-    return keys[max(p0, ts.gs + 1) - 1];   // unused when p0 == gs (a head)
-}
-
-template <typename KeyT>
-__device__ __forceinline__ KeyT prev_key(const KeyT (&x)[TileOf<KeyT>::per], int it, int lane, KeyT first_prev) {
-    const KeyT up = wave_shfl(x[it], 0, true);
-    const KeyT last = it ? wave_shfl(x[it > 0 ? it - 1 : 0], 63, false) : first_prev;
-    return lane ? up : last;
-}
-
-// ---- 3a. run heads per tile (into hist row 0)
-template <typename KeyT>
-__global__ void __launch_bounds__(kSBlock) sp_heads_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
-                                                           uint32_t* tfirst, int n, uint32_t* heads) {
-    using T = TileOf<KeyT>;
-    __shared__ uint32_t wsum[kSWaves];
-    TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // every load first (slot and predecessor; indices clamped into the tile / genome)
-    KeyT x[T::per];
-    const KeyT fp = load_keys(keys, ts, w, lane, x);
-    uint32_t c = 0;
-    bool disorder = false;
-#pragma unroll
-    for (int it = 0; it < T::per; ++it) {
-        const uint32_t li = w * T::wave_span + it * 64 + lane, p = ts.base + li;
-        const KeyT y = prev_key(x, it, lane, fp);
-        if (li < ts.cnt) {
-            c += p == ts.gs || x[it] != y ? 1u : 0u;
-            disorder |= p > ts.gs && x[it] < y;
-        }
-    }
-    if (__ballot(disorder) && (threadIdx.x & 63) == 0) atomicOr(&tfirst[n + 1], 2u);   // the sort's self-check
-    for (int d = 32; d >= 1; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) heads[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-}
-
-// ---- 3b. heads -> unique keys and their first slots (genome-relative)
-template <typename KeyT>
-__global__ void __launch_bounds__(kSBlock) sp_unique_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
-                                                            const uint32_t* tfirst, int n, const uint32_t* heads,
-                                                            uint64_t* __restrict__ ukeys, uint32_t* __restrict__ upos) {
-    using T = TileOf<KeyT>;
-    __shared__ uint32_t wsum[kSWaves];
-    TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, T::tile)) return;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t lt = (1ull << lane) - 1;
-    static_assert(T::per <= 64, "head flags: one bit per slot of the lane");
-    uint64_t hm = 0;   // head flags of this lane's slots
-    uint32_t mine = 0;
-    KeyT x[T::per];
-    {
-        const KeyT fp = load_keys(keys, ts, w, lane, x);
+        for (int it = 0; it < T::per; ++it) key[it] = in[ts.base + min(w * T::wave_span + it * 64 + lane, ts.cnt - 1)];
 #pragma unroll
         for (int it = 0; it < T::per; ++it) {
-            const uint32_t li = w * T::wave_span + it * 64 + lane, p = ts.base + li;
-            const KeyT y = prev_key(x, it, lane, fp);
-            const bool h = li < ts.cnt && (p == ts.gs || x[it] != y);
-            hm |= (h ? 1ull : 0ull) << it;
-            mine += (uint32_t)__popcll(__ballot(h));
-        }
-    }
-    if (lane == 0) wsum[w] = mine;
-    __syncthreads();
-    uint32_t u = heads[blockIdx.x];
-    for (int x = 0; x < w; ++x) u += wsum[x];
-#pragma unroll
-    for (int it = 0; it < T::per; ++it) {
-        const bool h = (hm >> it) & 1u;
-        const uint64_t b = __ballot(h);
-        if (h) {
             const uint32_t li = w * T::wave_span + it * 64 + lane;
-            const uint32_t j = u + (uint32_t)__popcll(b & lt);
-            ukeys[ts.gs + j] = (uint64_t)x[it];
-            upos[ts.gs + j] = ts.base + li - ts.gs;
+            const uint32_t d = (uint32_t)(key[it] >> shift) & dmask;
+            rank[it] = li < ts.cnt ? atomicAdd(&wc[w][d], 1u) : 0u;
         }
-        u += (uint32_t)__popcll(b);
+        __syncthreads();
+        {
+            const int d = tid;   // one digit per thread (bits <= 8)
+            const uint32_t c0 = wc[0][d], c1 = wc[1][d], c2 = wc[2][d], c3 = wc[3][d];
+            const bool live = d <= (int)dmask;
+            const uint32_t tot = c0 + c1 + c2 + c3;
+            const uint32_t gt = live ? gtot[ts.g * 256 + d] : 0u;
+            const uint32_t before =
+                live ? lookback(status + (uint64_t)d, 256, &tfirst[n + 1], t, tfirst[ts.g], tot, epoch) : 0u;
+            const uint32_t lb = block_excl_scan<kSWaves>(tot, wsum);
+            const uint32_t gb = block_excl_scan<kSWaves>(gt, wsum);
+            wc[0][d] = 0;
+            wc[1][d] = c0;
+            wc[2][d] = c0 + c1;
+            wc[3][d] = c0 + c1 + c2;
+            lbase[d] = lb;
+            gdst[d] = live ? ts.gs + gb + before - lb : 0u;
+        }
+        __syncthreads();
+        for (int it = 0; it < T::per; ++it) {
+            const uint32_t li = w * T::wave_span + it * 64 + lane;
+            if (li < ts.cnt) {
+                const uint32_t d = (uint32_t)(key[it] >> shift) & dmask;
+                stage[lbase[d] + wc[w][d] + rank[it]] = key[it];
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < ts.cnt; i += kSBlock) {
+            const KeyT x = stage[i];
+            out[gdst[(uint32_t)(x >> shift) & dmask] + i] = x;
+        }
+        __syncthreads();   // stage, gdst and tix are reused by the next tile
     }
 }
 
-// ---- 3c. counts = distance to the next head; tiles index unique slots here
-template <uint32_t Span>
-__global__ void __launch_bounds__(kSBlock) sp_counts_kernel(const uint64_t* goff, const uint32_t* tfirst, int n,
-                                                            const uint32_t* nfull, const uint32_t* upos,
-                                                            uint32_t* __restrict__ counts) {
-    constexpr int per = Span / kSBlock;
-    TileSpan ts;
-    if (!tile_span(goff, tfirst, n, blockIdx.x, ts, Span)) return;
-    const uint32_t nf = nfull[ts.g * 256];
-    const uint32_t len = ts.ge - ts.gs;
-    const uint32_t u0 = ts.base - ts.gs;   // the tile's first unique index
-    if (u0 >= nf) return;
-    const uint32_t* up = upos + ts.gs;
-    uint32_t a[per], b[per];
-#pragma unroll
-    for (int it = 0; it < per; ++it) {   // every load first (indices clamped below nf)
-        const uint32_t u = min(u0 + it * kSBlock + threadIdx.x, nf - 1);
-        a[it] = up[u];
-        b[it] = up[min(u + 1, nf - 1)];
-    }
-#pragma unroll
-    for (int it = 0; it < per; ++it) {
-        const uint32_t i = it * kSBlock + threadIdx.x, u = u0 + i;
-        if (i < ts.cnt && u < nf) counts[ts.gs + u] = (u + 1 < nf ? b[it] : len) - a[it];
-    }
-}
+// ============================================================================
+// Round-5 form: A count, B scatter by bucket, C chunk sort in LDS
+// ============================================================================
 
-// ---- 3d. distinct k-mers per genome (SENT dropped)
+// ---- A. genome x bucket totals.  Workgroup (g, y) takes every gridDim.y-th
+// tile of genome g (a whole row of counts per workgroup keeps the global adds
+// few: one per bucket per workgroup).
 template <typename KeyT>
-__global__ void __launch_bounds__(256) sp_nuniq_kernel(const KeyT* keys, const uint64_t* goff, int n,
-                                                       const uint32_t* nfull, const uint32_t* tfirst, KeyT sent,
-                                                       uint64_t* nuniq) {
+__global__ void __launch_bounds__(kBBlock) sp2_count_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
+                                                            const uint32_t* tfirst, int n, const uint64_t* excl,
+                                                            uint32_t n_excl, const uint32_t* xlo, int k, int bshift,
+                                                            uint32_t* gtot) {
+    __shared__ uint32_t h[kNB];
+    if (tfirst[n + 1] & 1u) return;   // invalid goff: nothing is counted
+    const int g = blockIdx.x;
+    const uint32_t t0 = tfirst[g], t1 = tfirst[g + 1];
+    if (t0 + blockIdx.y >= t1) return;   // uniform
+    for (uint32_t i = threadIdx.x; i < kNB; i += kBBlock) h[i] = 0;
+    __syncthreads();
+    const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
+    for (uint32_t t = t0 + blockIdx.y; t < t1; t += gridDim.y) {
+        TileSpan ts;
+        tile_span(goff, tfirst, n, t, ts, kTB);
+        KeyT out[kEB];
+#pragma unroll
+        for (int j = 0; j < kEB; ++j) out[j] = sent;
+        emit_row(bytes, ts, t, n_excl, excl, xlo, k, out);
+#pragma unroll
+        for (int j = 0; j < kEB; ++j)
+            if (out[j] != sent) atomicAdd(&h[(uint32_t)(out[j] >> bshift)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kNB; i += kBBlock)
+        if (h[i]) atomicAdd(&gtot[(uint64_t)g * kNB + i], h[i]);
+}
+
+// ---- A'. per genome: gbase[g][b] = goff[g] + keys of buckets < b; gkeys[g] = all
+__global__ void __launch_bounds__(1024) sp2_gbase_kernel(const uint64_t* goff, const uint32_t* gtot, int n,
+                                                         uint32_t* gbase, uint32_t* gkeys) {
+    __shared__ uint32_t wsum[16];
+    const int g = blockIdx.x;
+    const uint32_t v = gtot[(uint64_t)g * kNB + threadIdx.x];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<16>(v, wsum, &tot);
+    gbase[(uint64_t)g * kNB + threadIdx.x] = (uint32_t)goff[g] + ex;
+    if (threadIdx.x == 0) gkeys[g] = tot;
+}
+
+// ---- B. scatter by bucket.  Persistent workgroups (one per CU: 128 KiB of
+// staging for u64 keys) take tiles by ticket; per tile: the keys again from the
+// bytes (32 per thread, in registers), ranks by packed u16 LDS adds into the
+// wave's bucket counters, a tile-local scan, the look-back of each bucket over
+// the genome's earlier tiles, the tile re-ordered in LDS by bucket, and every
+// bucket's keys written as one run at gbase[g][b] + the earlier tiles' keys.
+template <typename KeyT>
+__global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
+                                                              uint32_t* tfirst, int n, const uint64_t* excl,
+                                                              uint32_t n_excl, const uint32_t* xlo, int k,
+                                                              int bshift, const uint32_t* gbase, uint64_t* status,
+                                                              uint32_t* ticket, const uint32_t* order,
+                                                              KeyT* __restrict__ out) {
+    __shared__ uint32_t wc[kBWaves][kNB / 2];   // per wave: packed u16 bucket counts, then the wave's base
+    __shared__ uint32_t lbase[kNB];             // tile-local start of each bucket
+    __shared__ uint32_t gdst[kNB];              // slot of the bucket's first key in this tile, minus lbase
+    __shared__ uint32_t wsum[kBWaves];
+    __shared__ uint32_t tix, nvalid;
+    extern __shared__ __attribute__((aligned(16))) uint8_t sp_dyn[];
+    KeyT* stage = (KeyT*)sp_dyn;   // kTB keys
+    const int tid = threadIdx.x, w = tid >> 6;
+    const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
+    const uint32_t nbe = 1u << sp_dbits(k);
+    for (;;) {
+        if (tid == 0) {
+            const uint32_t x = atomicAdd(ticket, 1u);
+            tix = order && x < tfirst[n] ? order[x] : x;
+        }
+        __syncthreads();
+        const uint32_t t = tix;
+        TileSpan ts;
+        if (!tile_span(goff, tfirst, n, t, ts, kTB)) return;   // uniform: no tiles left
+        KeyT key[kEB];
+#pragma unroll
+        for (int j = 0; j < kEB; ++j) key[j] = sent;
+        emit_row(bytes, ts, t, n_excl, excl, xlo, k, key);
+        for (int i = tid; i < kBWaves * (int)kNB / 2; i += kBBlock) (&wc[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t rk[kEB];
+#pragma unroll
+        for (int j = 0; j < kEB; ++j) {
+            const uint32_t b = (uint32_t)(key[j] >> bshift), sh = (b & 1u) << 4;
+            rk[j] = key[j] != sent ? (atomicAdd(&wc[w][b >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
+        }
+        __syncthreads();
+        {
+            // thread tid: buckets 2 tid, 2 tid + 1 (word tid of every wave's row)
+            uint32_t run = 0;
+#pragma unroll
+            for (int x = 0; x < kBWaves; ++x) {   // packed: both halves stay below 2^16
+                const uint32_t c = wc[x][tid];
+                wc[x][tid] = run;
+                run += c;
+            }
+            const uint32_t t0c = run & 0xFFFFu, t1c = run >> 16;
+            uint32_t all;
+            const uint32_t ex = block_excl_scan<kBWaves>(t0c + t1c, wsum, &all);
+            const uint32_t b0 = 2u * (uint32_t)tid, b1 = b0 + 1u;
+            lbase[b0] = ex;
+            lbase[b1] = ex + t0c;
+            const uint32_t tf = tfirst[ts.g];
+            uint32_t bf0 = 0, bf1 = 0;
+            if (b0 < nbe) bf0 = lookback(status + b0, kNB, &tfirst[n + 1], t, tf, t0c, 1u);
+            if (b1 < nbe) bf1 = lookback(status + b1, kNB, &tfirst[n + 1], t, tf, t1c, 1u);
+            gdst[b0] = b0 < nbe ? gbase[(uint64_t)ts.g * kNB + b0] + bf0 - ex : 0u;
+            gdst[b1] = b1 < nbe ? gbase[(uint64_t)ts.g * kNB + b1] + bf1 - (ex + t0c) : 0u;
+            if (tid == 0) nvalid = all;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kEB; ++j) {
+            if (key[j] != sent) {
+                const uint32_t b = (uint32_t)(key[j] >> bshift), sh = (b & 1u) << 4;
+                stage[lbase[b] + ((wc[w][b >> 1] >> sh) & 0xFFFFu) + rk[j]] = key[j];
+            }
+        }
+        __syncthreads();
+        const uint32_t nv = nvalid;
+        for (uint32_t i = tid; i < nv; i += kBBlock) {
+            const KeyT x = stage[i];
+            out[gdst[(uint32_t)(x >> bshift)] + i] = x;
+        }
+        __syncthreads();   // stage, gdst, tix are reused by the next tile
+    }
+}
+
+// ---- C0. chunk plan, one wave per genome.  Buckets are taken in order and
+// grouped greedily into chunks of at most cap keys; a bucket of more than cap
+// keys is a chunk of its own, sorted in the overflow area.  mode 0 counts
+// (nch, nbig, bigkeys per genome); mode 1 writes the chunks at cfirst[g] (and
+// the chunk -> genome map at cfirst[n + 2 + c]), the big chunks' overflow slots
+// at seg_off[bfirst[g] + i] and their chunk ids at bigc[].
+__global__ void __launch_bounds__(64) sp2_plan_kernel(const uint32_t* gtot, const uint32_t* gbase, int n, int k,
+                                                      uint32_t cap, int mode, uint32_t* nch, uint32_t* nbig,
+                                                      uint32_t* bigkeys, uint32_t* cfirst, const uint32_t* bfirst,
+                                                      const uint32_t* obase, Chunk* chunks, uint64_t* seg_off,
+                                                      uint32_t* bigc) {
+    const int g = blockIdx.x, lane = threadIdx.x;
+    const uint32_t nbe = 1u << sp_dbits(k);
+    uint32_t nc = 0, nb = 0, bk = 0;   // chunks, big chunks, big keys so far (wave-uniform)
+    uint32_t cur_lo = 0, cur_hi = 0, cur_n = 0;
+    const uint32_t c0 = mode ? cfirst[g] : 0u, bf0 = mode ? bfirst[g] : 0u, ob0 = mode ? obase[g] : 0u;
+    auto emit = [&](uint32_t lo, uint32_t hi, uint32_t cnt, bool big) {
+        if (mode && lane == 0) {
+            Chunk c;
+            c.start = gbase[(uint64_t)g * kNB + lo];
+            c.nkeys = cnt;
+            c.blo = (uint16_t)lo;
+            c.nb = (uint16_t)(hi - lo);
+            c.ovf = big ? ob0 + bk : kNoOvf;
+            chunks[c0 + nc] = c;
+            cfirst[n + 2 + c0 + nc] = (uint32_t)g;
+            if (big) {
+                seg_off[bf0 + nb] = ob0 + bk;
+                bigc[bf0 + nb] = c0 + nc;
+            }
+        }
+        ++nc;
+        if (big) {
+            ++nb;
+            bk += cnt;
+        }
+    };
+    for (uint32_t b0 = 0; b0 < nbe; b0 += 64) {
+        const uint32_t v = b0 + lane < nbe ? gtot[(uint64_t)g * kNB + b0 + lane] : 0u;
+        for (int i = 0; i < 64 && b0 + i < nbe; ++i) {
+            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, i), b = b0 + i;
+            if (c == 0) continue;
+            if (c > cap) {
+                if (cur_n) emit(cur_lo, cur_hi, cur_n, false);
+                cur_n = 0;
+                emit(b, b + 1, c, true);
+            } else if (cur_n + c > cap) {
+                emit(cur_lo, cur_hi, cur_n, false);
+                cur_lo = b;
+                cur_hi = b + 1;
+                cur_n = c;
+            } else {
+                if (!cur_n) cur_lo = b;
+                cur_hi = b + 1;
+                cur_n += c;
+            }
+        }
+    }
+    if (cur_n) emit(cur_lo, cur_hi, cur_n, false);
+    if (!mode && lane == 0) {
+        nch[g] = nc;
+        nbig[g] = nb;
+        bigkeys[g] = bk;
+    }
+}
+
+// ---- C0'. prefixes over genomes (one workgroup): cfirst (chunks; total at [n],
+// [n + 1] = 0), bfirst (big chunks), obase (overflow keys); the unused overflow
+// segments [big total, smax] are empty at the end of the area.
+__global__ void __launch_bounds__(1024) sp2_cscan_kernel(const uint32_t* nch, const uint32_t* nbig,
+                                                         const uint32_t* bigkeys, int n, uint32_t smax,
+                                                         uint32_t* cfirst, uint32_t* bfirst, uint32_t* obase,
+                                                         uint64_t* seg_off) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry[3];
+    if (threadIdx.x < 3) carry[threadIdx.x] = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += 1024) {
+        const int g = base + (int)threadIdx.x;
+        const uint32_t a = g < n ? nch[g] : 0u, b = g < n ? nbig[g] : 0u, c = g < n ? bigkeys[g] : 0u;
+        uint32_t ta, tb, tc;
+        const uint32_t ea = block_excl_scan<16>(a, wsum, &ta);
+        const uint32_t eb = block_excl_scan<16>(b, wsum, &tb);
+        const uint32_t ec = block_excl_scan<16>(c, wsum, &tc);
+        if (g < n) {
+            cfirst[g] = carry[0] + ea;
+            bfirst[g] = carry[1] + eb;
+            obase[g] = carry[2] + ec;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            carry[0] += ta;
+            carry[1] += tb;
+            carry[2] += tc;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        cfirst[n] = carry[0];
+        cfirst[n + 1] = 0;
+        bfirst[n] = carry[1];
+        obase[n] = carry[2];
+    }
+    for (uint32_t i = carry[1] + threadIdx.x; i <= smax; i += 1024) seg_off[i] = carry[2];
+}
+
+// ---- C1. big buckets -> the overflow area (workgroups loop over the big chunks)
+template <typename KeyT>
+__global__ void __launch_bounds__(256) sp2_gather_kernel(const KeyT* __restrict__ kb, const Chunk* chunks,
+                                                         const uint32_t* bigc, const uint32_t* bfirst, int n,
+                                                         KeyT* __restrict__ ovf) {
+    const uint32_t nbig = bfirst[n];
+    for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
+        const Chunk c = chunks[bigc[i]];
+        for (uint32_t j = threadIdx.x; j < c.nkeys; j += 256) ovf[c.ovf + j] = kb[c.start + j];
+    }
+}
+
+__device__ __forceinline__ uint32_t ceil_log2(uint32_t x) { return x <= 1 ? 0u : 32u - (uint32_t)__builtin_clz(x - 1); }
+
+// ---- C2. chunk sort + run-length encoding (persistent, one 512-thread
+// workgroup per CU).  A chunk's keys (minus its first bucket's base: R = B +
+// ceil(log2 nb) bits) are sorted in LDS by stable LSD passes of 8 bits: per
+// pass a returning packed-u16 LDS add per key into its wave's digit counter
+// (stable: an LDS unit serves one instruction's lanes in lane order, and keys
+// are striped so lane, then iteration, then wave is slot order), one wave scans
+// the 256 x 16 counters, the keys go to their slots in LDS and come back
+// striped.  Then each thread takes `per` consecutive sorted keys: head flags
+// (a key unlike its predecessor) into an LDS bit mask, a block scan numbers the
+// heads, the chunk learns the genome's distinct k-mers before it by look-back,
+// and every head writes (key, distance to the next head).
+template <typename KeyT>
+__global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restrict__ kb, const KeyT* __restrict__ ovf,
+                                                            const Chunk* chunks, const uint32_t* cfirst, int n,
+                                                            int bshift, const uint64_t* goff, uint32_t* flags,
+                                                            uint64_t* cstatus, uint32_t* ticket,
+                                                            const uint32_t* order, uint64_t* __restrict__ okeys,
+                                                            uint32_t* __restrict__ ocounts, uint64_t* unq) {
+    using CO = ChunkOf<KeyT>;
+    constexpr int PER = CO::per;
+    __shared__ uint32_t wc[kCWaves][128];   // packed u16 digit counters per wave; the head bit mask after the sort
+    __shared__ uint32_t dbase[256];
+    __shared__ uint32_t wsum[kCWaves];
+    __shared__ uint32_t cid, before_s;
+    extern __shared__ __attribute__((aligned(16))) uint8_t sp_dyn[];
+    KeyT* stage = (KeyT*)sp_dyn;   // cap keys
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (;;) {
+        if (tid == 0) {
+            const uint32_t x = atomicAdd(ticket, 1u);
+            cid = order && x < cfirst[n] ? order[x] : x;
+        }
+        __syncthreads();
+        const uint32_t c = cid;
+        if (c >= cfirst[n]) return;   // uniform
+        const uint32_t g = cfirst[n + 2 + c];
+        const Chunk ch = chunks[c];
+        const uint32_t c0 = cfirst[g];
+        const bool last = c + 1 == cfirst[g + 1];
+        const uint64_t obase = goff[g];
+        const uint32_t nk = ch.nkeys;
+        if (ch.ovf == kNoOvf) {
+            // ------------------------------------------------ in-LDS sort
+            const KeyT base = (KeyT)ch.blo << bshift;
+            const uint32_t R = (uint32_t)bshift + ceil_log2(ch.nb);
+            const int passes = (int)((R + 7) / 8);
+            // striped slot li0 + 64 it; `rem` keeps the 32 bounds tests from holding 32 slot registers
+            uint32_t li0 = (uint32_t)w * CO::wave_span + (uint32_t)lane;
+            asm volatile("" : "+v"(li0));   // per chunk: nothing derived from it is hoisted out of the loop
+            const int rem = (int)nk - (int)li0;
+            const KeyT* src = kb + ch.start + li0;
+            KeyT* srow = stage + li0;
+            KeyT y[PER];
+#pragma unroll
+            for (int it = 0; it < PER; ++it)   // padding sorts last (all ones below R bits and above)
+                y[it] = it * 64 < rem ? (KeyT)(src[it * 64] - base) : (KeyT)~(KeyT)0;
+            if (passes == 0) {
+#pragma unroll
+                for (int it = 0; it < PER; ++it) srow[it * 64] = y[it];
+            }
+            for (int p = 0; p < passes; ++p) {
+                const int sh8 = 8 * p;
+                for (int i = tid; i < kCWaves * 128; i += kCBlock) (&wc[0][0])[i] = 0;
+                __syncthreads();
+                uint32_t rk[PER];
+#pragma unroll
+                for (int it = 0; it < PER; ++it) {
+                    const uint32_t d = (uint32_t)(y[it] >> sh8) & 0xFFu, sh = (d & 1u) << 4;
+                    rk[it] = (atomicAdd(&wc[w][d >> 1], 1u << sh) >> sh) & 0xFFFFu;
+                }
+                __syncthreads();
+                if (w == 0) {   // lane: digits 4 lane .. 4 lane + 3 (words 2 lane, 2 lane + 1)
+                    uint32_t r0 = 0, r1 = 0;
+#pragma unroll
+                    for (int x = 0; x < kCWaves; ++x) {
+                        const uint32_t a = wc[x][2 * lane], b = wc[x][2 * lane + 1];
+                        wc[x][2 * lane] = r0;
+                        wc[x][2 * lane + 1] = r1;
+                        r0 += a;
+                        r1 += b;
+                    }
+                    const uint32_t d0 = r0 & 0xFFFFu, d1 = r0 >> 16, d2 = r1 & 0xFFFFu, d3 = r1 >> 16;
+                    const uint32_t s = d0 + d1 + d2 + d3;
+                    uint32_t inc = s;
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+                        if (lane >= d) inc += o;
+                    }
+                    const uint32_t ex = inc - s;
+                    dbase[4 * lane] = ex;
+                    dbase[4 * lane + 1] = ex + d0;
+                    dbase[4 * lane + 2] = ex + d0 + d1;
+                    dbase[4 * lane + 3] = ex + d0 + d1 + d2;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int it = 0; it < PER; ++it) {
+                    const uint32_t d = (uint32_t)(y[it] >> sh8) & 0xFFu, sh = (d & 1u) << 4;
+                    stage[dbase[d] + ((wc[w][d >> 1] >> sh) & 0xFFFFu) + rk[it]] = y[it];
+                }
+                __syncthreads();
+                if (p + 1 < passes) {
+#pragma unroll
+                    for (int it = 0; it < PER; ++it) y[it] = srow[it * 64];
+                }
+            }
+            __syncthreads();
+            // ------------------------------------------------ run-length encoding
+            const uint32_t i0 = (uint32_t)tid * PER;
+            uint32_t mask = 0;
+            bool disorder = false;
+            {
+                KeyT pv = i0 ? stage[i0 - 1] : (KeyT)0;
+#pragma unroll
+                for (int q = 0; q < PER; ++q) {
+                    const uint32_t i = i0 + q;
+                    const KeyT v = stage[i];
+                    if (i < nk) {
+                        mask |= (i == 0 || v != pv) ? 1u << q : 0u;
+                        disorder |= i > 0 && v < pv;
+                    }
+                    pv = v;
+                }
+            }
+            if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u);   // the sort's self-check
+            uint32_t* hm = &wc[0][0];   // head bits: word m = slots 32 m .. 32 m + 31
+            if constexpr (PER == 32) {
+                hm[tid] = mask;
+            } else {
+                static_assert(PER == 16, "16 or 32 keys per thread");
+                ((uint16_t*)hm)[tid] = (uint16_t)mask;   // little endian: slots 16 tid .. 16 tid + 15
+            }
+            uint32_t nu;
+            const uint32_t j0 = block_excl_scan<kCWaves>((uint32_t)__builtin_popcount(mask), wsum, &nu);
+            if (tid == 0) {
+                const uint32_t bf = lookback(cstatus, 1, flags, c, c0, nu, 1u);
+                before_s = bf;
+                if (last) unq[g] = (uint64_t)bf + nu;
+            }
+            __syncthreads();
+            uint64_t o = obase + before_s + j0;
+            for (uint32_t m = mask; m; m &= m - 1u, ++o) {   // this thread's heads, in order
+                const uint32_t q = (uint32_t)__builtin_ctz(m), i = i0 + q;
+                const uint32_t rest = m & (m - 1u);
+                uint32_t nx;
+                if (rest) {
+                    nx = i0 + (uint32_t)__builtin_ctz(rest);
+                } else {   // the first head after this thread's slots (bits past nk are 0)
+                    uint32_t pos = i0 + PER;
+                    nx = nk;
+                    while (pos < nk) {
+                        const uint32_t wd = hm[pos >> 5] >> (pos & 31u);
+                        if (wd) {
+                            nx = pos + (uint32_t)__builtin_ctz(wd);
+                            break;
+                        }
+                        pos = (pos | 31u) + 1u;
+                    }
+                }
+                okeys[o] = (uint64_t)(stage[i] + base);
+                ocounts[o] = min(nx, nk) - i;
+            }
+            __syncthreads();   // stage, wc, cid are reused by the next chunk
+        } else {
+            // ------------------------------------------------ big bucket (sorted in the overflow area)
+            const KeyT* x = ovf + ch.ovf;
+            uint32_t cnt = 0;
+            bool disorder = false;
+            for (uint32_t i = tid; i < nk; i += kCBlock) {
+                const KeyT a = x[i], pv = i ? x[i - 1] : a;
+                cnt += (i == 0 || a != pv) ? 1u : 0u;
+                disorder |= a < pv;
+            }
+            if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u);
+            uint32_t nu;
+            (void)block_excl_scan<kCWaves>(cnt, wsum, &nu);
+            if (tid == 0) {
+                const uint32_t bf = lookback(cstatus, 1, flags, c, c0, nu, 1u);
+                before_s = bf;
+                if (last) unq[g] = (uint64_t)bf + nu;
+            }
+            __syncthreads();
+            const uint64_t o0 = obase + before_s;
+            // heads in order: key and (temporarily) its slot
+            uint32_t run = 0;
+            for (uint32_t r = 0; r < nk; r += kCBlock) {
+                const uint32_t i = r + (uint32_t)tid;
+                const KeyT a = i < nk ? x[i] : (KeyT)0, pv = i && i < nk ? x[i - 1] : a;
+                const bool hd = i < nk && (i == 0 || a != pv);
+                uint32_t tot;
+                const uint32_t e = block_excl_scan<kCWaves>(hd ? 1u : 0u, wsum, &tot);
+                if (hd) {
+                    okeys[o0 + run + e] = (uint64_t)a;
+                    ocounts[o0 + run + e] = i;
+                }
+                run += tot;
+            }
+            // counts = next head's slot - this one's (reads before writes, per round)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            for (uint32_t r = 0; r < nu; r += kCBlock) {
+                const uint32_t jj = r + (uint32_t)tid;
+                uint32_t a = 0, b = 0;
+                if (jj < nu) {
+                    a = __builtin_nontemporal_load(ocounts + o0 + jj);
+                    b = jj + 1 < nu ? __builtin_nontemporal_load(ocounts + o0 + jj + 1) : nk;
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (jj < nu) ocounts[o0 + jj] = b - a;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+        }
+    }
+}
+
+// ---- C3. distinct k-mers per genome (the last chunk's inclusive prefix; 0
+// for a genome without windows) or the failure codes.
+__global__ void __launch_bounds__(256) sp2_final_kernel(const uint32_t* tfirst, int n, const uint32_t* oflags,
+                                                        const uint64_t* unq, uint64_t* nuniq) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
-    if (tfirst[n + 1] & 1u) {   // invalid goff (sp_tiles_kernel): nothing was counted
-        nuniq[g] = ~0ull;
-        return;
-    }
-    if (tfirst[n + 1] & 2u) {   // the final order check failed (sp_heads_kernel)
-        nuniq[g] = ~1ull;
-        return;
-    }
-    uint32_t nf = nfull[g * 256];
-    const uint64_t ge = goff[g + 1];
-    if (nf > 0 && keys[ge - 1] == sent) --nf;
-    nuniq[g] = nf;
+    const uint32_t f = tfirst[n + 1] | (*oflags & 2u);
+    nuniq[g] = (f & 1u) ? ~0ull : (f & 2u) ? ~1ull : unq[g];
 }
 
 // Workspace carve-up (byte offsets, 256-aligned).
 struct SpLayout {
-    uint64_t tfirst, xlo, keys, hist, gtot, upos, gall, ticket, order, total;   // hist doubles as the look-back status
-    uint32_t hstride;
+    // phase A / B: tiles of kTB bytes
+    uint64_t tfirst, xlo, gtot, gbase, gkeys, bstatus, bticket, border;
+    // phase C: chunks
+    uint64_t nch, nbig, bigkeys, cfirst, bfirst, obase, chunks, bigc, cstatus, cticket, corder, unq;
+    // overflow LSD sort of big buckets
+    uint64_t seg_off, otfirst, oxlo, ostatus, ogall, oticket, oorder;
+    uint64_t kb, ovf, total;   // bucketed keys, overflow keys
+    uint32_t tiles, cmax, smax, otiles;
 };
 
 uint64_t al256(uint64_t x) { return (x + 255) & ~255ull; }
@@ -834,40 +1000,77 @@ uint64_t al256(uint64_t x) { return (x + 255) & ~255ull; }
 SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
     SpLayout L;
     const uint64_t ks = k <= 16 ? 4 : 8;
-    L.hstride = (uint32_t)(batch_bytes / tile_for_k(k) + (uint64_t)n + 1);
+    const uint64_t cap = 16384;   // ChunkOf<KeyT>::cap
+    L.tiles = (uint32_t)(batch_bytes / kTB + (uint64_t)n + 1);
+    // greedy packing: two consecutive chunks hold more than cap keys together
+    L.cmax = (uint32_t)(2 * batch_bytes / cap + (uint64_t)n + 1);
+    L.smax = (uint32_t)(batch_bytes / (cap + 1) + 1);   // big buckets hold more than cap keys
+    L.otiles = (uint32_t)(batch_bytes / (ks == 4 ? TileOf<uint32_t>::tile : TileOf<uint64_t>::tile) + L.smax + 1);
+    const uint64_t nn = (uint64_t)n;
     uint64_t o = 0;
-    L.tfirst = o;   // tfirst[0..n], the flags word, then the tile -> genome map
-    o = al256(o + 4ull * ((uint64_t)n + 2 + L.hstride));
-    L.xlo = o;
-    o = al256(o + 4ull * ((uint64_t)L.hstride + 1));
-    L.keys = o;
-    o = al256(o + ks * batch_bytes);
-    L.hist = o;
-    o = al256(o + (KF_SPARSE_LOOKBACK ? 8ull : 4ull) * 256 * L.hstride);
-    L.gtot = o;
-    o = al256(o + 4ull * 256 * (uint64_t)n);
-    L.upos = o;
-    o = al256(o + 4ull * batch_bytes);
-    L.gall = o;   // passes x n x 256 genome digit counts (look-back)
-    o = al256(o + 4ull * 8 * 256 * (uint64_t)n);
-    L.ticket = o;   // a tile counter per pass
-    o = al256(o + 4ull * 8);
-    L.order = o;    // ticket -> tile
-    o = al256(o + 4ull * L.hstride);
+    auto put = [&](uint64_t& f, uint64_t bytes) {
+        f = o;
+        o = al256(o + bytes);
+    };
+    put(L.tfirst, 4ull * (nn + 2 + L.tiles));
+    put(L.xlo, 4ull * (L.tiles + 1));
+    put(L.gtot, 4ull * nn * kNB);
+    put(L.gbase, 4ull * nn * kNB);
+    put(L.gkeys, 4ull * nn);
+    put(L.bstatus, 8ull * kNB * L.tiles);
+    put(L.bticket, 4ull * 4);
+    put(L.border, 4ull * L.tiles);
+    put(L.nch, 4ull * nn);
+    put(L.nbig, 4ull * nn);
+    put(L.bigkeys, 4ull * nn);
+    put(L.cfirst, 4ull * (nn + 2 + L.cmax));
+    put(L.bfirst, 4ull * (nn + 1));
+    put(L.obase, 4ull * (nn + 1));
+    put(L.chunks, sizeof(Chunk) * (uint64_t)L.cmax);
+    put(L.bigc, 4ull * L.smax);
+    put(L.cstatus, 8ull * L.cmax);
+    put(L.cticket, 4ull * 4);
+    put(L.corder, 4ull * L.cmax);
+    put(L.unq, 8ull * nn);
+    put(L.seg_off, 8ull * (L.smax + 1));
+    put(L.otfirst, 4ull * (L.smax + 2 + L.otiles));
+    put(L.oxlo, 4ull * (L.otiles + 1));
+    put(L.ostatus, 8ull * 256 * L.otiles);
+    put(L.ogall, 4ull * 8 * 256 * L.smax);
+    put(L.oticket, 4ull * 8);
+    put(L.oorder, 4ull * L.otiles);
+    put(L.kb, ks * batch_bytes);
+    put(L.ovf, ks * batch_bytes);
     L.total = o;
     return L;
 }
 
 template <typename KeyT>
-int sp_prepare() {   // the scatter's staging tile is dynamic LDS (64 KiB for u64 keys)
+int sp_prepare() {   // dynamic LDS: phase B staging, phase C chunk, LSD staging
     static bool done = false;
     if (done) return KF_OK;
-    if (hipFuncSetAttribute((const void*)&sp_scatter_kernel<KeyT, KF_SPARSE_LOOKBACK != 0>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)&sp2_scatter_kernel<KeyT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(kTB * sizeof(KeyT))) != hipSuccess ||
+        hipFuncSetAttribute((const void*)&sp2_chunk_kernel<KeyT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(ChunkOf<KeyT>::cap * sizeof(KeyT))) != hipSuccess ||
+        hipFuncSetAttribute((const void*)&sp_scatter_kernel<KeyT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(TileOf<KeyT>::tile * sizeof(KeyT))) != hipSuccess)
         return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     done = true;
     return KF_OK;
+}
+
+int sp_cus() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0)
+            cus = c;
+        else
+            cus = 256;
+    }
+    return cus;
 }
 
 template <typename KeyT>
@@ -875,71 +1078,105 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
            uint64_t n_excl, int k, uint8_t* work, const SpLayout& L, uint64_t* d_keys, uint32_t* d_counts,
            uint64_t* d_nuniq, hipStream_t s) {
     if (const int rc = sp_prepare<KeyT>()) return rc;
-    uint32_t* tfirst = (uint32_t*)(work + L.tfirst);
-    KeyT* kw = (KeyT*)(work + L.keys);     // the sorted keys end here
-    KeyT* ka = (KeyT*)d_keys;              // d_keys doubles as the other sort buffer
-    uint32_t* hist = (uint32_t*)(work + L.hist);
-    uint32_t* gtot = (uint32_t*)(work + L.gtot);
-    uint32_t* upos = (uint32_t*)(work + L.upos);
-    const uint32_t grid = L.hstride;       // >= the batch's tile count
-    const int bits_total = 2 * k;
-    const int passes = (bits_total + 7) / 8;
-    const int bits = (bits_total + passes - 1) / passes;
-    hipLaunchKernelGGL(sp_tiles_kernel, dim3(1), dim3(1024), 0, s, d_goff, n, batch_bytes, TileOf<KeyT>::tile, tfirst);
-    uint32_t* xlo = (uint32_t*)(work + L.xlo);
-    hipLaunchKernelGGL(sp_tilemap_kernel, dim3(grid / 256 + 1), dim3(256), 0, s, d_goff, tfirst, n, d_excl,
-                       (uint32_t)n_excl, TileOf<KeyT>::tile, xlo);
-    // the last pass must write kw: start in kw for an even number of passes
-    KeyT* src = (passes % 2 == 0) ? kw : ka;
-    KeyT* dst = (passes % 2 == 0) ? ka : kw;
-    hipLaunchKernelGGL(sp_emit_kernel<KeyT>, dim3(grid), dim3(TileOf<KeyT>::emit_threads), 0, s, d_bytes, d_goff, tfirst, n, d_excl,
-                       (uint32_t)n_excl, xlo, k, src);
-#if KF_SPARSE_LOOKBACK
-    uint64_t* status = (uint64_t*)(work + L.hist);
-    uint32_t* gall = (uint32_t*)(work + L.gall);
-    uint32_t* ticket = (uint32_t*)(work + L.ticket);
-    if (hipMemsetAsync(status, 0, 8ull * 256 * L.hstride, s) != hipSuccess ||
-        hipMemsetAsync(gall, 0, L.order - L.gall, s) != hipSuccess)   // gall and the tickets
+    auto at32 = [&](uint64_t off) { return (uint32_t*)(work + off); };
+    uint32_t* tfirst = at32(L.tfirst);
+    uint32_t* xlo = at32(L.xlo);
+    const int D = sp_dbits(k), B = 2 * k - D;
+    const int cus = sp_cus();
+    // clear what is accumulated or polled: bucket totals, look-back words, tickets
+    if (hipMemsetAsync(work + L.gtot, 0, 4ull * n * kNB, s) != hipSuccess ||
+        hipMemsetAsync(work + L.bstatus, 0, L.border - L.bstatus, s) != hipSuccess ||   // status + ticket
+        hipMemsetAsync(work + L.cstatus, 0, L.corder - L.cstatus, s) != hipSuccess ||   // status + ticket
+        hipMemsetAsync(work + L.unq, 0, 8ull * n, s) != hipSuccess ||
+        hipMemsetAsync(work + L.ostatus, 0, L.oorder - L.ostatus, s) != hipSuccess)     // status, gall, tickets
         return kf_fail(KF_EHIP, "memset failed");
-    const uint32_t slices = (uint32_t)max(1, min(1024, 4096 / max(1, (int)n)));
-    hipLaunchKernelGGL(sp_ghist_kernel<KeyT>, dim3((uint32_t)n, slices), dim3(kSBlock), 0, s, src, d_goff, tfirst, n,
-                       passes, bits, gall);
-    uint32_t* order = nullptr;
+    // tiles of kTB bytes per genome, their genome and first excluded range
+    hipLaunchKernelGGL(sp_tiles_kernel, dim3(1), dim3(1024), 0, s, d_goff, n, batch_bytes, kTB, tfirst);
+    hipLaunchKernelGGL(sp_tilemap_kernel, dim3(L.tiles / 256 + 1), dim3(256), 0, s, d_goff, tfirst, n, d_excl,
+                       (uint32_t)n_excl, kTB, xlo);
+    // A: genome x bucket totals
+    const uint32_t slices = (uint32_t)max(1, min(64, 1024 / max(1, (int)n)));
+    hipLaunchKernelGGL(sp2_count_kernel<KeyT>, dim3((uint32_t)n, slices), dim3(kBBlock), 0, s, d_bytes, d_goff, tfirst,
+                       n, d_excl, (uint32_t)n_excl, xlo, k, B, at32(L.gtot));
+    hipLaunchKernelGGL(sp2_gbase_kernel, dim3((uint32_t)n), dim3(1024), 0, s, d_goff, at32(L.gtot), n, at32(L.gbase),
+                       at32(L.gkeys));
+    // B: scatter by bucket
+    uint32_t* border = nullptr;
     if (n > 1 && n <= KF_SPARSE_ORDER_MAXN) {
-        order = (uint32_t*)(work + L.order);
-        hipLaunchKernelGGL(sp_order_kernel, dim3((grid + kSBlock - 1) / kSBlock), dim3(kSBlock), 0, s, tfirst, n, order);
+        border = at32(L.border);
+        hipLaunchKernelGGL(sp_order_kernel, dim3(L.tiles / kSBlock + 1), dim3(kSBlock), 0, s, tfirst, n, border);
     }
-#endif
-    for (int p = 0; p < passes; ++p) {
-        const int shift = p * bits;
-        const int b = min(bits, bits_total - shift);
-#if KF_SPARSE_LOOKBACK
-        hipLaunchKernelGGL((sp_scatter_kernel<KeyT, true>), dim3(grid), dim3(kSBlock), TileOf<KeyT>::tile * sizeof(KeyT),
-                           s, src, dst, d_goff, tfirst, n, shift, b, nullptr, L.hstride,
-                           gall + (uint64_t)p * n * 256, status, ticket + p, (uint32_t)p + 1, order);
-#else
-        hipLaunchKernelGGL(sp_hist_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, src, d_goff, tfirst, n, shift, b,
-                           hist, L.hstride);
-        hipLaunchKernelGGL(sp_scan_kernel, dim3((uint32_t)n, 1u << b), dim3(kSBlock), 0, s, hist, L.hstride, tfirst,
-                           gtot);
-        hipLaunchKernelGGL((sp_scatter_kernel<KeyT, false>), dim3(grid), dim3(kSBlock), TileOf<KeyT>::tile * sizeof(KeyT),
-                           s, src, dst, d_goff, tfirst, n, shift, b, hist, L.hstride, gtot, nullptr, nullptr, 0u,
-                           nullptr);
-#endif
-        KeyT* t = src;
-        src = dst;
-        dst = t;
+    KeyT* kb = (KeyT*)(work + L.kb);
+    KeyT* ovf = (KeyT*)(work + L.ovf);
+    hipLaunchKernelGGL(sp2_scatter_kernel<KeyT>, dim3((uint32_t)cus), dim3(kBBlock), kTB * sizeof(KeyT), s, d_bytes,
+                       d_goff, tfirst, n, d_excl, (uint32_t)n_excl, xlo, k, B, at32(L.gbase),
+                       (uint64_t*)(work + L.bstatus), at32(L.bticket), border, kb);
+    // C0: chunk plan
+    const uint32_t cap = ChunkOf<KeyT>::cap;
+    uint64_t* seg_off = (uint64_t*)(work + L.seg_off);
+    hipLaunchKernelGGL(sp2_plan_kernel, dim3((uint32_t)n), dim3(64), 0, s, at32(L.gtot), at32(L.gbase), n, k, cap, 0,
+                       at32(L.nch), at32(L.nbig), at32(L.bigkeys), at32(L.cfirst), at32(L.bfirst), at32(L.obase),
+                       (Chunk*)(work + L.chunks), seg_off, at32(L.bigc));
+    hipLaunchKernelGGL(sp2_cscan_kernel, dim3(1), dim3(1024), 0, s, at32(L.nch), at32(L.nbig), at32(L.bigkeys), n,
+                       L.smax, at32(L.cfirst), at32(L.bfirst), at32(L.obase), seg_off);
+    hipLaunchKernelGGL(sp2_plan_kernel, dim3((uint32_t)n), dim3(64), 0, s, at32(L.gtot), at32(L.gbase), n, k, cap, 1,
+                       at32(L.nch), at32(L.nbig), at32(L.bigkeys), at32(L.cfirst), at32(L.bfirst), at32(L.obase),
+                       (Chunk*)(work + L.chunks), seg_off, at32(L.bigc));
+    // C1: big buckets -> overflow area, LSD-sorted there on their low B bits
+    // (nothing to do, and every workgroup leaves at once, unless a bucket
+    // holds more than cap keys)
+    const int passes = (B + 7) / 8;
+    if (passes > 0) {
+        const int bits = (B + passes - 1) / passes;
+        // the sorted keys must end in ovf: gather into ovf for an even number of passes
+        KeyT* src = (passes % 2 == 0) ? ovf : (KeyT*)d_keys;
+        KeyT* dst = (passes % 2 == 0) ? (KeyT*)d_keys : ovf;
+        hipLaunchKernelGGL(sp2_gather_kernel<KeyT>, dim3((uint32_t)cus), dim3(256), 0, s, kb,
+                           (const Chunk*)(work + L.chunks), at32(L.bigc), at32(L.bfirst), n, src);
+        uint32_t* otfirst = at32(L.otfirst);
+        const int S = (int)L.smax;
+        hipLaunchKernelGGL(sp_tiles_kernel, dim3(1), dim3(1024), 0, s, seg_off, S, batch_bytes, TileOf<KeyT>::tile,
+                           otfirst);
+        hipLaunchKernelGGL(sp_tilemap_kernel, dim3(L.otiles / 256 + 1), dim3(256), 0, s, seg_off, otfirst, S,
+                           (const uint64_t*)nullptr, 0u, TileOf<KeyT>::tile, at32(L.oxlo));
+        uint32_t* gall = at32(L.ogall);
+        hipLaunchKernelGGL(sp_ghist_kernel<KeyT>, dim3((uint32_t)min(S, 4 * cus)), dim3(kSBlock), 0, s, src, seg_off,
+                           otfirst, S, passes, bits, gall);
+        uint32_t* oorder = nullptr;
+        if (S > 1 && S <= KF_SPARSE_ORDER_MAXN) {
+            oorder = at32(L.oorder);
+            hipLaunchKernelGGL(sp_order_kernel, dim3(L.otiles / kSBlock + 1), dim3(kSBlock), 0, s, otfirst, S, oorder);
+        }
+        for (int p = 0; p < passes; ++p) {
+            const int shift = p * bits;
+            const int b = min(bits, B - shift);
+            hipLaunchKernelGGL(sp_scatter_kernel<KeyT>, dim3((uint32_t)(2 * cus)), dim3(kSBlock),
+                               TileOf<KeyT>::tile * sizeof(KeyT), s, src, dst, seg_off, otfirst, S, shift, b,
+                               gall + (uint64_t)p * S * 256, (uint64_t*)(work + L.ostatus), at32(L.oticket) + p,
+                               (uint32_t)p + 1, oorder);
+            KeyT* t = src;
+            src = dst;
+            dst = t;
+        }
+    } else {
+        // B == 0 (k <= 5): a bucket is one key value; a big bucket is sorted as it stands
+        hipLaunchKernelGGL(sp2_gather_kernel<KeyT>, dim3((uint32_t)cus), dim3(256), 0, s, kb,
+                           (const Chunk*)(work + L.chunks), at32(L.bigc), at32(L.bfirst), n, ovf);
     }
-    // src == kw: sorted
-    hipLaunchKernelGGL(sp_heads_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, kw, d_goff, tfirst, n, hist);
-    hipLaunchKernelGGL(sp_scan_kernel, dim3((uint32_t)n, 1), dim3(kSBlock), 0, s, hist, L.hstride, tfirst, gtot);
-    hipLaunchKernelGGL(sp_unique_kernel<KeyT>, dim3(grid), dim3(kSBlock), 0, s, kw, d_goff, tfirst, n, hist, d_keys,
-                       upos);
-    hipLaunchKernelGGL(sp_counts_kernel<TileOf<KeyT>::tile>, dim3(grid), dim3(kSBlock), 0, s, d_goff, tfirst, n, gtot,
-                       upos, d_counts);
-    const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
-    hipLaunchKernelGGL(sp_nuniq_kernel<KeyT>, dim3((n + 255) / 256), dim3(256), 0, s, kw, d_goff, n, gtot, tfirst, sent,
-                       d_nuniq);
+    // C2: chunks
+    uint32_t* corder = nullptr;
+    if (n > 1 && n <= KF_SPARSE_ORDER_MAXN) {
+        corder = at32(L.corder);
+        hipLaunchKernelGGL(sp_order_kernel, dim3(L.cmax / kSBlock + 1), dim3(kSBlock), 0, s, at32(L.cfirst), n, corder);
+    }
+    hipLaunchKernelGGL(sp2_chunk_kernel<KeyT>, dim3((uint32_t)cus), dim3(kCBlock), ChunkOf<KeyT>::cap * sizeof(KeyT), s,
+                       kb, ovf, (const Chunk*)(work + L.chunks), at32(L.cfirst), n, B, d_goff, &tfirst[n + 1],
+                       (uint64_t*)(work + L.cstatus), at32(L.cticket), corder, d_keys, d_counts,
+                       (uint64_t*)(work + L.unq));
+    // the overflow sort's flag word (look-back stall) when it ran, else the main one
+    const uint32_t* oflags = passes > 0 ? at32(L.otfirst) + L.smax + 1 : &tfirst[n + 1];
+    hipLaunchKernelGGL(sp2_final_kernel, dim3((n + 255) / 256), dim3(256), 0, s, tfirst, n, oflags,
+                       (const uint64_t*)(work + L.unq), d_nuniq);
     return KF_OK;
 }
 

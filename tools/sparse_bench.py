@@ -49,6 +49,9 @@ def main() -> None:
         try:
             g0 = sc.to_host(keys[: int(off[1])], cnts[: int(off[1])], nu[:1], off[:2])[0]
             ok = int(g0[1].sum(dtype=np.uint64)) == a.seq_len - k + 1
+            import kf_oracle as O
+            ek, ec = O.sparse_count(db.data[int(off[0]): int(off[1])].cpu().numpy().tobytes(), k)
+            ok = ok and bool(np.array_equal(g0[0], ek) and np.array_equal(g0[1], ec))
         except Exception as e:   # profiling ablation builds (KF_SPARSE_ABL) sort wrongly by design
             ok = f"no: {e}"
         med = float(np.median(ms))
