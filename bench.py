@@ -520,7 +520,10 @@ def sparse_bench(args, dev) -> dict:
     after one warm launch.  Genome 0 is checked against the oracle's restatement
     and every genome's total against seq_len - k + 1 (outside the timing).
     `roofline.achieved` counts the algorithmic bytes (FASTA read + 12 B per
-    distinct k-mer written); the sort itself moves ~24 B per key per 8-bit pass."""
+    distinct k-mer written); the design moves the input twice (bucket count,
+    bucket scatter), each key once out and once back in (the bucketed keys), and
+    12 B per distinct k-mer out (round 5; round 4's LSD sort moved ~2 x 8 B per
+    key per 8-bit pass)."""
     import torch
     from kf2vecfsw_amd import counter as C
     k, n, L = args.sparse_k, args.sparse_genomes, args.seq_len
@@ -551,8 +554,9 @@ def sparse_bench(args, dev) -> dict:
         tot[g] = c64[int(off[g]): int(off[g]) + int(nuh[g])].sum()
     ok &= bool((tot.cpu().numpy() == L - k + 1).all())
     alg = nbytes + 12 * int(nuh.sum())
-    passes = (2 * k + 7) // 8
     key_b = 4 if k <= 16 else 8
+    bucket_bits = min(10, 2 * k)
+    lds_passes = (2 * k - bucket_bits + 2 + 7) // 8   # a chunk spans ~2-4 buckets
     del keys, cnts, nu, db, sc, tot, c64
     torch.cuda.empty_cache()
     return {"config": f"get_kmers sparse counter, k={k}, {n} synthetic {L / 1e6:g} Mbp genomes resident in HBM "
@@ -562,9 +566,10 @@ def sparse_bench(args, dev) -> dict:
             "roofline": {"bound": "hbm", "achieved": round(alg / (med * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBPS,
                          "unit": "GB/s", "frac": round(alg / (med * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
                          "alg_bytes_per_launch": alg,
-                         "design_bytes_per_launch": int(n * L * (1 + 2 * key_b + passes * 2 * key_b + 6 * key_b)),
-                         "note": f"LSD radix sort of {2 * k}-bit keys: emit, one digit count, {passes} single-sweep "
-                                 f"passes of 2 x {key_b} B per key, run-length encoding"},
+                         "design_bytes_per_launch": int(nbytes * 2 + n * L * 2 * key_b + 12 * int(nuh.sum())),
+                         "note": f"{2 * k}-bit keys: bucket count over the bytes, bucket scatter ({key_b} B per key "
+                                 f"out, top {bucket_bits} bits), per-chunk LDS sort ({lds_passes} passes of 8 bits "
+                                 f"in LDS, {key_b} B per key in) + run-length encoding (12 B per distinct k-mer out)"},
             "parity": "ok" if ok else "MISMATCH"}
 
 

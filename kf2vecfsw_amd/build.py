@@ -70,6 +70,21 @@ def build(force: bool = False, verbose: bool = False, ablation: bool = False, ou
         return _build_locked(verbose, ablation, out)
 
 
+HEADERS = ["kf_internal.h", "kf_front.h", "../../include/kf2vec_gpu.h"]
+
+
+def _object(src: str, cmd_tail: list[str]) -> tuple[str, bool]:
+    """Object path for `src` compiled with `cmd_tail`, keyed by the hash of the
+    source, the shared headers and the command (so an edit rebuilds only the
+    objects it touches); and whether it already exists."""
+    h = hashlib.sha256(" ".join(cmd_tail).encode())
+    for d in [src] + HEADERS:
+        with open(os.path.join(CSRC, d), "rb") as f:
+            h.update(f.read())
+    o = os.path.join(BUILD, f"{src}.{h.hexdigest()[:16]}.o")
+    return o, os.path.exists(o)
+
+
 def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
     objs = []
     # profiling / ablation builds carry a suffix, so the product check refuses them
@@ -77,18 +92,22 @@ def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
     bid = source_id() + ("+prof" if ablation else "") + \
         ("+flags" + hashlib.sha256(flags.encode()).hexdigest()[:8] if flags.strip() else "")
     for s in SOURCES_HIP:
-        o = os.path.join(BUILD, s + ".o")
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-c", os.path.join(CSRC, s), "-o", o] + (["-DKF_PROFILE_BUILD"] if ablation else [])
-        cmd += os.environ.get("KF_HIPCC_FLAGS", "").split()   # tools/ only (profiling ablations)
-        if verbose:
-            cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
-        subprocess.run(cmd, check=True)
+        tail = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"] + \
+            (["-DKF_PROFILE_BUILD"] if ablation else []) + flags.split()   # KF_HIPCC_FLAGS: tools/ only
+        o, have = _object(s, tail)
+        if not have or verbose:
+            cmd = [HIPCC] + tail + ["-c", os.path.join(CSRC, s), "-o", o + ".tmp"]
+            if verbose:
+                cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
+            subprocess.run(cmd, check=True)
+            os.replace(o + ".tmp", o)
         objs.append(o)
     for s in SOURCES_CPP:
-        o = os.path.join(BUILD, s + ".o")
-        subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-pthread",
-                        f'-DKF_BUILD_ID="{bid}"', "-c", os.path.join(CSRC, s), "-o", o], check=True)
+        tail = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-pthread", f'-DKF_BUILD_ID="{bid}"']
+        o, have = _object(s, tail)
+        if not have:
+            subprocess.run(["g++"] + tail + ["-c", os.path.join(CSRC, s), "-o", o + ".tmp"], check=True)
+            os.replace(o + ".tmp", o)
         objs.append(o)
     tmp = out + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs, "-o", tmp],

@@ -130,10 +130,12 @@ def pack_genomes(blobs: Sequence[bytes | np.ndarray], names: Sequence[str] | Non
 
 def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: int = N.KF_FMT_AUTO,
                pin: bool = True, threads: int = 8, pool=None, times: dict | None = None,
-               buf: torch.Tensor | None = None, index: bool = True) -> HostBatch:
-    """Read files straight into one (pinned) buffer and index their records; files
-    are read and indexed by a thread pool (readinto and the ctypes call release the
-    GIL): `pool` if given (shared across batches), else one of `threads` workers.
+               buf: torch.Tensor | None = None, index: bool = True, piece: int = 1 << 20) -> HostBatch:
+    """Read files straight into one (pinned) buffer and index their records; the
+    reads are cut into pieces of at most `piece` bytes (os.preadv at the piece's
+    offset) run by a thread pool (the syscalls and the ctypes index calls release
+    the GIL), so a batch of a few large files still keeps every worker reading:
+    `pool` if given (shared across batches), else one of `threads` workers.
     `buf`: a caller-owned (pinned) buffer of at least the batch's bytes to read
     into instead of a fresh allocation (the caller makes sure no copy still reads it).
     index=False: a batch of FASTA files is not indexed here (excl None: to_device
@@ -151,29 +153,43 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
     d = data.numpy()
     if times is not None:
         times["alloc_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    piece = max(1 << 16, int(piece))
+    tasks = [(i, a, min(sizes[i], a + piece)) for i in range(len(paths)) for a in range(0, sizes[i], piece)]
+    fds = [os.open(p, os.O_RDONLY) for p in paths]
 
-    def one(i: int) -> np.ndarray:
+    def read(t) -> None:
+        i, a, e = t
+        lo = int(off[i])
+        mv = memoryview(d[lo + a: lo + e])
+        got = 0
+        while got < e - a:
+            n = os.preadv(fds[i], [mv[got:]], a + got)
+            if not n:
+                raise IOError(f"short read on {paths[i]}")
+            got += n
+
+    def host_index(i: int):
         lo, sz = int(off[i]), sizes[i]
-        with open(paths[i], "rb", buffering=0) as f:
-            got = 0
-            mv = memoryview(d[lo: lo + sz])
-            while got < sz:
-                n = f.readinto(mv[got:])
-                if not n:
-                    raise IOError(f"short read on {paths[i]}")
-                got += n
         d[lo + sz: int(off[i + 1])] = 10
         if not index and fmt != N.KF_FMT_FASTQ and not (fmt == N.KF_FMT_AUTO and sz > 0 and d[lo] == ord("@")):
             return None   # FASTA: the device indexes it
         return index_records(d[lo: lo + sz], fmt, lo)[0]
 
-    if pool is not None:
-        excl = list(pool.map(one, range(len(paths))))
-    elif threads > 1 and len(paths) > 1:
-        with ThreadPoolExecutor(max_workers=min(threads, len(paths))) as ex:
-            excl = list(ex.map(one, range(len(paths))))
-    else:
-        excl = [one(i) for i in range(len(paths))]
+    try:
+        if pool is not None:
+            list(pool.map(read, tasks))
+            excl = list(pool.map(host_index, range(len(paths))))
+        elif threads > 1 and len(tasks) > 1:
+            with ThreadPoolExecutor(max_workers=min(threads, len(tasks))) as ex:
+                list(ex.map(read, tasks))
+                excl = list(ex.map(host_index, range(len(paths))))
+        else:
+            for t in tasks:
+                read(t)
+            excl = [host_index(i) for i in range(len(paths))]
+    finally:
+        for fd in fds:
+            os.close(fd)
     if not index and all(e is None for e in excl):
         return HostBatch(data, off, None, list(names) if names else list(paths))
     excl = [e if e is not None else index_records(d[int(off[i]): int(off[i]) + sizes[i]], N.KF_FMT_FASTA,

@@ -344,6 +344,20 @@ inline char* raw_columns(const CT* c, uint64_t n, int m, char* p, uint64_t* zero
 
 uint64_t kf_line_cap(size_t name_len, uint64_t nbins) { return name_len + 2 + nbins * 26; }
 
+// Per-thread memo of one row's normalised column texts by count (format_line).
+struct NormMemo {
+    static constexpr uint32_t kMemo = 4096;   // counts memoised (larger ones are formatted each time)
+    static constexpr uint32_t kSlot = 24;     // bytes copied per column: repr of a double is <= 24 chars
+    uint32_t row = 0;                         // generation of the current row
+    uint32_t gen[kMemo] = {};
+    uint8_t len[kMemo];
+    char txt[kMemo][kSlot];
+};
+NormMemo& norm_memo() {
+    thread_local std::unique_ptr<NormMemo> m(new NormMemo);   // ~120 KB per formatting thread
+    return *m;
+}
+
 // main.py:327-357
 template <typename T>
 uint64_t format_line(const char* name, const T* c, uint64_t nb, int pseudo, int raw, char* out) {
@@ -372,10 +386,27 @@ uint64_t format_line(const char* name, const T* c, uint64_t nb, int pseudo, int 
         for (uint64_t i = 0; i < nb; ++i) usum += c[i];
         double sum = (double)usum;              // exact: integers < 2^53
         if (pseudo) sum += 0.5 * (double)nb;   // exact: multiples of 0.5 < 2^53
+        // A row holds few distinct counts (k=7, 5 Mbp: ~1-2 thousand values over
+        // 8,192 columns), and a column's text depends on its count only: each
+        // count below kMemo is formatted once per row and copied after that.
+        NormMemo& M = norm_memo();
+        if (++M.row == 0) {   // generation counter wrapped: forget every entry
+            memset(M.gen, 0, sizeof M.gen);
+            M.row = 1;
+        }
         for (uint64_t i = 0; i < nb; ++i) {
             if (i) *p++ = ',';
-            const double v = ((double)c[i] + (pseudo ? 0.5 : 0.0)) / sum;
-            p = fmt_repr(v, p);
+            const uint32_t ci = (uint32_t)c[i];
+            if (ci < NormMemo::kMemo) {
+                if (M.gen[ci] != M.row) {
+                    M.gen[ci] = M.row;
+                    M.len[ci] = (uint8_t)(fmt_repr(((double)ci + (pseudo ? 0.5 : 0.0)) / sum, M.txt[ci]) - M.txt[ci]);
+                }
+                memcpy(p, M.txt[ci], NormMemo::kSlot);   // the row buffer has >= 26 B per column
+                p += M.len[ci];
+            } else {
+                p = fmt_repr(((double)ci + (pseudo ? 0.5 : 0.0)) / sum, p);
+            }
         }
     }
     *p++ = '\n';

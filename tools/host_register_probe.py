@@ -66,6 +66,31 @@ def main():
         out["read_pinned_1thread"] = {"read_s": round(r[0], 4), "read_GBps": gbps(r[0]), "h2d_s": round(r[1], 4),
                                       "h2d_GBps": gbps(r[1])}
 
+        # per-thread read rate into pageable vs pinned memory, and 16 threads into pinned
+        from concurrent.futures import ThreadPoolExecutor
+        pageable = np.empty(total, dtype=np.uint8)
+
+        def read_into(d, i):
+            with open(paths[i], "rb", buffering=0) as f:
+                f.readinto(memoryview(d[i * size:(i + 1) * size]))
+
+        for name, d in (("pageable", pageable), ("pinned", pinned.numpy())):
+            ts = []
+            for _ in range(a.reps):
+                t0 = time.perf_counter()
+                for i in range(len(paths)):
+                    read_into(d, i)
+                ts.append(time.perf_counter() - t0)
+            out[f"read_1thread_{name}_GBps"] = gbps(min(ts))
+        for nt in (4, 8, 16):
+            ts = []
+            with ThreadPoolExecutor(nt) as ex:
+                for _ in range(a.reps):
+                    t0 = time.perf_counter()
+                    list(ex.map(lambda i: read_into(pinned.numpy(), i), range(len(paths))))
+                    ts.append(time.perf_counter() - t0)
+            out[f"read_{nt}threads_pinned_GBps"] = gbps(min(ts))
+
         # mmap + hipHostRegister + H2D per file + unregister
         res = []
         for _ in range(a.reps):
