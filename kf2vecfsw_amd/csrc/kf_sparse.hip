@@ -777,7 +777,6 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
     using CO = ChunkOf<KeyT>;
     constexpr int PER = CO::per;
     __shared__ uint32_t wc[kCWaves][128];   // packed u16 digit counters per wave; the head bit mask after the sort
-    __shared__ uint32_t dbase[256];
     __shared__ uint32_t wsum[kCWaves];
     __shared__ uint32_t cid, before_s;
     extern __shared__ __attribute__((aligned(16))) uint8_t sp_dyn[];
@@ -801,7 +800,6 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             // ------------------------------------------------ in-LDS sort
             const KeyT base = (KeyT)ch.blo << bshift;
             const uint32_t R = (uint32_t)bshift + ceil_log2(ch.nb);
-            const int passes = (int)((R + 7) / 8);
             // striped slot li0 + 64 it; `rem` keeps the 32 bounds tests from holding 32 slot registers
             uint32_t li0 = (uint32_t)w * CO::wave_span + (uint32_t)lane;
             asm volatile("" : "+v"(li0));   // per chunk: nothing derived from it is hoisted out of the loop
@@ -809,58 +807,131 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             const KeyT* src = kb + ch.start + li0;
             KeyT* srow = stage + li0;
             KeyT y[PER];
+            uint32_t rk[PER];
 #pragma unroll
             for (int it = 0; it < PER; ++it)   // padding sorts last (all ones below R bits and above)
                 y[it] = it * 64 < rem ? (KeyT)(src[it * 64] - base) : (KeyT)~(KeyT)0;
-            if (passes == 0) {
-#pragma unroll
-                for (int it = 0; it < PER; ++it) srow[it * 64] = y[it];
-            }
-            for (int p = 0; p < passes; ++p) {
-                const int sh8 = 8 * p;
+            // one stable pass by the 8-bit digit at bit sh8: keys y (striped) -> stage in digit order
+            auto pass = [&](int sh8, bool reload) __attribute__((always_inline)) {
                 for (int i = tid; i < kCWaves * 128; i += kCBlock) (&wc[0][0])[i] = 0;
                 __syncthreads();
-                uint32_t rk[PER];
 #pragma unroll
                 for (int it = 0; it < PER; ++it) {
                     const uint32_t d = (uint32_t)(y[it] >> sh8) & 0xFFu, sh = (d & 1u) << 4;
                     rk[it] = (atomicAdd(&wc[w][d >> 1], 1u << sh) >> sh) & 0xFFFFu;
                 }
                 __syncthreads();
-                if (w == 0) {   // lane: digits 4 lane .. 4 lane + 3 (words 2 lane, 2 lane + 1)
-                    uint32_t r0 = 0, r1 = 0;
+                if (w == 0) {
+                    // lane: digits 4 lane .. 4 lane + 3 (words 2 lane, 2 lane + 1 of every wave's
+                    // row).  Every counter becomes its keys' first slot: the digit's start
+                    // plus the counts of the earlier waves (packed halves: <= cap < 2^16).
+                    uint32_t a[kCWaves], b[kCWaves], r0 = 0, r1 = 0;
 #pragma unroll
                     for (int x = 0; x < kCWaves; ++x) {
-                        const uint32_t a = wc[x][2 * lane], b = wc[x][2 * lane + 1];
-                        wc[x][2 * lane] = r0;
-                        wc[x][2 * lane + 1] = r1;
-                        r0 += a;
-                        r1 += b;
+                        a[x] = wc[x][2 * lane];
+                        b[x] = wc[x][2 * lane + 1];
+                        r0 += a[x];
+                        r1 += b[x];
                     }
-                    const uint32_t d0 = r0 & 0xFFFFu, d1 = r0 >> 16, d2 = r1 & 0xFFFFu, d3 = r1 >> 16;
-                    const uint32_t s = d0 + d1 + d2 + d3;
-                    uint32_t inc = s;
+                    const uint32_t d0 = r0 & 0xFFFFu, d1 = r0 >> 16, d2 = r1 & 0xFFFFu;
+                    const uint32_t sum = d0 + d1 + d2 + (r1 >> 16);
+                    uint32_t inc = sum;
                     for (int d = 1; d < 64; d <<= 1) {
                         const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
                         if (lane >= d) inc += o;
                     }
-                    const uint32_t ex = inc - s;
-                    dbase[4 * lane] = ex;
-                    dbase[4 * lane + 1] = ex + d0;
-                    dbase[4 * lane + 2] = ex + d0 + d1;
-                    dbase[4 * lane + 3] = ex + d0 + d1 + d2;
+                    const uint32_t ex = inc - sum;
+                    uint32_t q0 = ex | ((ex + d0) << 16), q1 = (ex + d0 + d1) | ((ex + d0 + d1 + d2) << 16);
+#pragma unroll
+                    for (int x = 0; x < kCWaves; ++x) {
+                        wc[x][2 * lane] = q0;
+                        wc[x][2 * lane + 1] = q1;
+                        q0 += a[x];
+                        q1 += b[x];
+                    }
                 }
                 __syncthreads();
 #pragma unroll
                 for (int it = 0; it < PER; ++it) {
                     const uint32_t d = (uint32_t)(y[it] >> sh8) & 0xFFu, sh = (d & 1u) << 4;
-                    stage[dbase[d] + ((wc[w][d >> 1] >> sh) & 0xFFFFu) + rk[it]] = y[it];
+                    stage[((wc[w][d >> 1] >> sh) & 0xFFFFu) + rk[it]] = y[it];
                 }
                 __syncthreads();
-                if (p + 1 < passes) {
+                if (reload) {
 #pragma unroll
                     for (int it = 0; it < PER; ++it) y[it] = srow[it * 64];
                 }
+            };
+            // Round 0: for R > 16 the most significant 16 bits only (two passes): a chunk
+            // holds <= 16,384 keys over 65,536 values of those bits, so what is left
+            // unsorted is runs of a few keys with equal top bits, each sorted by one
+            // thread in LDS.  A run longer than kRun whose keys are not all equal
+            // (repeats make long runs of EQUAL keys, which need nothing) sends the chunk
+            // to round 1: every bit below R, least significant digit first (LSD sorts
+            // any order).  For R <= 16 round 0 is that full LSD.
+            constexpr uint32_t kRun = 32;
+            for (int round = 0; round < 2; ++round) {
+                const bool msd = round == 0 && R > 16;
+                const int lo = msd ? (int)R - 16 : 0;
+                const int np = msd ? 2 : (int)((R + 7) / 8);
+                if (np == 0) {   // one key value: already sorted
+#pragma unroll
+                    for (int it = 0; it < PER; ++it) srow[it * 64] = y[it];
+                    __syncthreads();
+                }
+                for (int p = 0; p < np; ++p) pass(lo + 8 * p, p + 1 < np);
+                if (!msd) break;
+                const uint32_t i0 = (uint32_t)tid * PER;
+                uint32_t sm = 0;   // run starts among this thread's slots
+                {
+                    KeyT pv = i0 ? stage[i0 - 1] >> lo : (KeyT)0;
+#pragma unroll
+                    for (int q = 0; q < PER; ++q) {
+                        const KeyT v = stage[i0 + q] >> lo;
+                        sm |= (i0 + q < nk && (i0 + q == 0 || v != pv)) ? 1u << q : 0u;
+                        pv = v;
+                    }
+                }
+                uint32_t* hm = &wc[0][0];
+                static_assert(PER == 32, "one mask word per thread");
+                hm[tid] = sm;
+                __syncthreads();
+                bool lng = false;
+                for (uint32_t m = sm; m; m &= m - 1u) {
+                    const uint32_t st = i0 + (uint32_t)__builtin_ctz(m), rest = m & (m - 1u);
+                    uint32_t en = nk;
+                    if (rest) {
+                        en = i0 + (uint32_t)__builtin_ctz(rest);
+                    } else {
+                        for (uint32_t pos = i0 + PER; pos < nk; pos = (pos | 31u) + 1u) {
+                            const uint32_t wd = hm[pos >> 5] >> (pos & 31u);
+                            if (wd) {
+                                en = pos + (uint32_t)__builtin_ctz(wd);
+                                break;
+                            }
+                        }
+                    }
+                    en = min(en, nk);
+                    if (en - st < 2) continue;
+                    if (en - st > kRun) {   // long: fine only if every key equals the first
+                        const KeyT f = stage[st];
+                        for (uint32_t i = st + 1; i < en && !lng; ++i) lng = stage[i] != f;
+                        continue;
+                    }
+                    for (uint32_t i = st + 1; i < en; ++i) {   // insertion sort (stable)
+                        const KeyT v = stage[i];
+                        uint32_t j = i;
+                        while (j > st && stage[j - 1] > v) {
+                            stage[j] = stage[j - 1];
+                            --j;
+                        }
+                        stage[j] = v;
+                    }
+                }
+                if (!__syncthreads_or(lng)) break;
+#pragma unroll
+                for (int it = 0; it < PER; ++it) y[it] = srow[it * 64];
+                __syncthreads();
             }
             __syncthreads();
             // ------------------------------------------------ run-length encoding

@@ -235,7 +235,7 @@ def get_frequencies(args) -> None:
             args.k, supported_k.start, supported_k.stop - 1))
 
     import torch
-    from .counter import KmerCounter, pack_files, to_device
+    from .counter import KmerCounter, pack_files, pack_files_registered, to_device
 
     if shard is not None and not os.environ.get("KF_SHARD"):
         # torchrun: join the host-only gloo group now, before counting, so that a
@@ -279,12 +279,23 @@ def get_frequencies(args) -> None:
     # n_slots once the H2D that last read that slot has completed
     slot_bytes = max(sum((os.path.getsize(paths[i]) + 15) // 16 * 16 for i in b) for b in batches)
     n_slots = min(len(batches), int(os.environ.get("KF_READ_AHEAD", "2")) + 2)
-    slots = [torch.empty(max(slot_bytes, 16), dtype=torch.uint8, pin_memory=True) for _ in range(n_slots)]
+    slots = [torch.empty(max(slot_bytes, 16), dtype=torch.uint8, pin_memory=True)
+             for _ in range(0 if os.environ.get("KF_READ_MODE") == "register" else n_slots)]
     slot_ev: list = [None] * n_slots
+
+    # KF_READ_MODE=register: the files' page-cache pages are page-locked in place
+    # and copied by the DMA engine (no host memcpy; counter.pack_files_registered)
+    register = os.environ.get("KF_READ_MODE") == "register"
 
     def pack(bi, idx):
         t0 = now_ms()
         tm = {}
+        if register:
+            hb = pack_files_registered([paths[i] for i in idx], [samples_names[i] for i in idx], device,
+                                       copy_stream)
+            if trace:
+                tr.append(("read", idx[0], t0, now_ms(), tm))
+            return hb
         j = bi % n_slots
         if slot_ev[j] is not None:
             slot_ev[j].synchronize()
@@ -334,8 +345,10 @@ def get_frequencies(args) -> None:
     # pinned count matrix (4 x bins B per genome), so the backlog is bounded
     behind = max(1, int(os.environ.get("KF_WRITE_BEHIND", "2")))
 
-    def write(ev, host, names):
+    def write(ev, host, names, reg):
         ev.synchronize()
+        if reg is not None:   # the batch's copies ran long ago (its count and copy-back have)
+            reg.release()
         t0 = now_ms()
         c = host.numpy().view(np.uint32)
         write_kf_files(args.output_dir, names, c, args.pseudocount, args.raw_cnt, args.p)
@@ -356,6 +369,7 @@ def get_frequencies(args) -> None:
                 e[0].record(stream)
                 evs.append((bi, now_ms(), e))
             db = to_device(hb, device)
+            reg = hb.reg
             del hb
             if trace:
                 e[1].record(stream)
@@ -382,7 +396,7 @@ def get_frequencies(args) -> None:
                 print(">>> Normalizing. Sample: {}".format(files_names[i]))
         if bi >= behind:   # backpressure: at most `behind` batches queued for the writer
             writes[bi - behind].result()
-        writes.append(writer.submit(write, ev, host, [samples_names[idx[j]] for j in keep]))
+        writes.append(writer.submit(write, ev, host, [samples_names[idx[j]] for j in keep], reg))
         del host, rows, counts, db
         if trace:
             th.append(now_ms())
