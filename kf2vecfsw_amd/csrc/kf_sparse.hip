@@ -881,37 +881,34 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 }
                 for (int p = 0; p < np; ++p) pass(lo + 8 * p, p + 1 < np);
                 if (!msd) break;
-                const uint32_t i0 = (uint32_t)tid * PER;
-                uint32_t sm = 0;   // run starts among this thread's slots
-                {
-                    KeyT pv = i0 ? stage[i0 - 1] >> lo : (KeyT)0;
-#pragma unroll
-                    for (int q = 0; q < PER; ++q) {
-                        const KeyT v = stage[i0 + q] >> lo;
-                        sm |= (i0 + q < nk && (i0 + q == 0 || v != pv)) ? 1u << q : 0u;
-                        pv = v;
+                // run starts: bit i of hm (ballots over striped slots: consecutive lanes,
+                // consecutive slots, so the LDS reads do not conflict)
+                uint32_t* hm = &wc[0][0];   // 512 words = slots 0 .. 16,383
+                static_assert(CO::cap == 32 * 512 && kCWaves * 128 >= 1024, "head mask + word prefix fit wc");
+#pragma unroll 4
+                for (int it = 0; it < PER; ++it) {
+                    const uint32_t i = li0 + (uint32_t)it * 64;
+                    const KeyT v = srow[it * 64] >> lo, pv = i ? stage[i - 1] >> lo : (KeyT)0;
+                    const uint64_t b64 = __ballot(i < nk && (i == 0 || v != pv));
+                    if (lane == 0) {
+                        hm[i >> 5] = (uint32_t)b64;
+                        hm[(i >> 5) + 1] = (uint32_t)(b64 >> 32);
                     }
                 }
-                uint32_t* hm = &wc[0][0];
-                static_assert(PER == 32, "one mask word per thread");
-                hm[tid] = sm;
                 __syncthreads();
                 bool lng = false;
-                for (uint32_t m = sm; m; m &= m - 1u) {
-                    const uint32_t st = i0 + (uint32_t)__builtin_ctz(m), rest = m & (m - 1u);
-                    uint32_t en = nk;
-                    if (rest) {
-                        en = i0 + (uint32_t)__builtin_ctz(rest);
-                    } else {
-                        for (uint32_t pos = i0 + PER; pos < nk; pos = (pos | 31u) + 1u) {
-                            const uint32_t wd = hm[pos >> 5] >> (pos & 31u);
-                            if (wd) {
-                                en = pos + (uint32_t)__builtin_ctz(wd);
-                                break;
-                            }
+#pragma unroll 4
+                for (int it = 0; it < PER; ++it) {
+                    const uint32_t st = li0 + (uint32_t)it * 64;
+                    if (st >= nk || !((hm[st >> 5] >> (st & 31u)) & 1u)) continue;
+                    uint32_t en = nk;   // the next run start (bits past nk are 0)
+                    for (uint32_t pos = st + 1; pos < nk; pos = (pos | 31u) + 1u) {
+                        const uint32_t wd = hm[pos >> 5] >> (pos & 31u);
+                        if (wd) {
+                            en = pos + (uint32_t)__builtin_ctz(wd);
+                            break;
                         }
                     }
-                    en = min(en, nk);
                     if (en - st < 2) continue;
                     if (en - st > kRun) {   // long: fine only if every key equals the first
                         const KeyT f = stage[st];
@@ -935,59 +932,54 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             }
             __syncthreads();
             // ------------------------------------------------ run-length encoding
-            const uint32_t i0 = (uint32_t)tid * PER;
-            uint32_t mask = 0;
+            // Striped again: head bit i = a key unlike its predecessor (ballots); word
+            // prefix counts number the heads; consecutive lanes hold consecutive slots,
+            // so the (key, count) stores of a wave are contiguous.
+            uint32_t* hm = &wc[0][0];        // head bits, 512 words
+            uint32_t* wpre = &wc[0][0] + 512;   // heads before each word
             bool disorder = false;
-            {
-                KeyT pv = i0 ? stage[i0 - 1] : (KeyT)0;
-#pragma unroll
-                for (int q = 0; q < PER; ++q) {
-                    const uint32_t i = i0 + q;
-                    const KeyT v = stage[i];
-                    if (i < nk) {
-                        mask |= (i == 0 || v != pv) ? 1u << q : 0u;
-                        disorder |= i > 0 && v < pv;
-                    }
-                    pv = v;
+#pragma unroll 4
+            for (int it = 0; it < PER; ++it) {
+                const uint32_t i = li0 + (uint32_t)it * 64;
+                const KeyT v = srow[it * 64], pv = i ? stage[i - 1] : (KeyT)0;
+                disorder |= i < nk && i > 0 && v < pv;
+                const uint64_t b64 = __ballot(i < nk && (i == 0 || v != pv));
+                if (lane == 0) {
+                    hm[i >> 5] = (uint32_t)b64;
+                    hm[(i >> 5) + 1] = (uint32_t)(b64 >> 32);
                 }
             }
             if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u);   // the sort's self-check
-            uint32_t* hm = &wc[0][0];   // head bits: word m = slots 32 m .. 32 m + 31
-            if constexpr (PER == 32) {
-                hm[tid] = mask;
-            } else {
-                static_assert(PER == 16, "16 or 32 keys per thread");
-                ((uint16_t*)hm)[tid] = (uint16_t)mask;   // little endian: slots 16 tid .. 16 tid + 15
-            }
+            __syncthreads();
             uint32_t nu;
-            const uint32_t j0 = block_excl_scan<kCWaves>((uint32_t)__builtin_popcount(mask), wsum, &nu);
+            {
+                const uint32_t wd = hm[tid];   // 512 threads, one word each
+                wpre[tid] = block_excl_scan<kCWaves>((uint32_t)__builtin_popcount(wd), wsum, &nu);
+            }
             if (tid == 0) {
                 const uint32_t bf = lookback(cstatus, 1, flags, c, c0, nu, 1u);
                 before_s = bf;
                 if (last) unq[g] = (uint64_t)bf + nu;
             }
             __syncthreads();
-            uint64_t o = obase + before_s + j0;
-            for (uint32_t m = mask; m; m &= m - 1u, ++o) {   // this thread's heads, in order
-                const uint32_t q = (uint32_t)__builtin_ctz(m), i = i0 + q;
-                const uint32_t rest = m & (m - 1u);
-                uint32_t nx;
-                if (rest) {
-                    nx = i0 + (uint32_t)__builtin_ctz(rest);
-                } else {   // the first head after this thread's slots (bits past nk are 0)
-                    uint32_t pos = i0 + PER;
-                    nx = nk;
-                    while (pos < nk) {
-                        const uint32_t wd = hm[pos >> 5] >> (pos & 31u);
-                        if (wd) {
-                            nx = pos + (uint32_t)__builtin_ctz(wd);
-                            break;
-                        }
-                        pos = (pos | 31u) + 1u;
+            const uint64_t o0 = obase + before_s;
+#pragma unroll 4
+            for (int it = 0; it < PER; ++it) {
+                const uint32_t i = li0 + (uint32_t)it * 64;
+                if (i >= nk) continue;
+                const uint32_t wd = hm[i >> 5];
+                if (!((wd >> (i & 31u)) & 1u)) continue;
+                const uint32_t j = wpre[i >> 5] + (uint32_t)__builtin_popcount(wd & ((1u << (i & 31u)) - 1u));
+                uint32_t nx = nk;
+                for (uint32_t pos = i + 1; pos < nk; pos = (pos | 31u) + 1u) {
+                    const uint32_t w2 = hm[pos >> 5] >> (pos & 31u);
+                    if (w2) {
+                        nx = pos + (uint32_t)__builtin_ctz(w2);
+                        break;
                     }
                 }
-                okeys[o] = (uint64_t)(stage[i] + base);
-                ocounts[o] = min(nx, nk) - i;
+                okeys[o0 + j] = (uint64_t)(srow[it * 64] + base);
+                ocounts[o0 + j] = min(nx, nk) - i;
             }
             __syncthreads();   // stage, wc, cid are reused by the next chunk
         } else {
