@@ -88,6 +88,17 @@ int kf_index_records(const uint8_t* bytes, uint64_t len, int fmt, uint64_t base,
                      uint64_t* out_iv, uint64_t cap_pairs, uint64_t* n_pairs,
                      int* fmt_detected);
 
+/* Read n files into one host buffer (replaces the per-file open/read that the
+ * reference leaves to Jellyfish, main.py:309-311): file i (sizes[i] bytes,
+ * checked against the file) goes to dst + off[i], and the bytes
+ * [off[i] + sizes[i], off[i+1]) are set to '\n' (transparent padding).  The reads
+ * are cut into pieces of at most `piece` bytes (pread) shared by n_threads native
+ * threads, so a few large files still keep every thread reading; no Python (or
+ * its interpreter lock) runs per piece.  KF_EINVAL on an unreadable or
+ * resized file (the message names it). */
+int kf_read_files(const char* const* paths, int32_t n, const uint64_t* sizes, const uint64_t* off,
+                  uint8_t* dst, uint64_t piece, int n_threads);
+
 /* The FASTA record index of a batch resident in HBM (what kf_index_records finds
  * per file, found on the device so the host only copies the files): the header
  * lines -- a line starting with '>' at a genome start or after '\n', up to its

@@ -132,11 +132,11 @@ def pack_genomes(blobs: Sequence[bytes | np.ndarray], names: Sequence[str] | Non
 def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: int = N.KF_FMT_AUTO,
                pin: bool = True, threads: int = 8, pool=None, times: dict | None = None,
                buf: torch.Tensor | None = None, index: bool = True, piece: int = 1 << 20) -> HostBatch:
-    """Read files straight into one (pinned) buffer and index their records; the
-    reads are cut into pieces of at most `piece` bytes (os.preadv at the piece's
-    offset) run by a thread pool (the syscalls and the ctypes index calls release
-    the GIL), so a batch of a few large files still keeps every worker reading:
-    `pool` if given (shared across batches), else one of `threads` workers.
+    """Read files straight into one (pinned) buffer and index their records.  The
+    bytes come from one native call (kf_read_files: pieces of at most `piece`
+    bytes read by pread on native threads, as many as `pool` has workers or
+    `threads`); FASTQ files (and FASTA ones when index=True) are then indexed by
+    the pool (the ctypes index calls release the GIL).
     `buf`: a caller-owned (pinned) buffer of at least the batch's bytes to read
     into instead of a fresh allocation (the caller makes sure no copy still reads it).
     index=False: a batch of FASTA files is not indexed here (excl None: to_device
@@ -154,43 +154,31 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
     d = data.numpy()
     if times is not None:
         times["alloc_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
-    piece = max(1 << 16, int(piece))
-    tasks = [(i, a, min(sizes[i], a + piece)) for i in range(len(paths)) for a in range(0, sizes[i], piece)]
-    fds = [os.open(p, os.O_RDONLY) for p in paths]
+    # the bytes: one native call (kf_read_files: pread pieces on native threads)
+    nthr = getattr(pool, "_max_workers", None) or max(1, int(threads))
+    if paths:
+        enc = [os.fsencode(p) for p in paths]
+        arr = (ctypes.c_char_p * len(enc))(*enc)
+        sz = np.asarray(sizes, dtype=np.uint64)
+        N.check(N.lib().kf_read_files(arr, len(enc), sz.ctypes.data, off.ctypes.data, d.ctypes.data,
+                                      int(piece), int(nthr)), "kf_read_files")
 
-    def read(t) -> None:
-        i, a, e = t
-        lo = int(off[i])
-        mv = memoryview(d[lo + a: lo + e])
-        got = 0
-        while got < e - a:
-            n = os.preadv(fds[i], [mv[got:]], a + got)
-            if not n:
-                raise IOError(f"short read on {paths[i]}")
-            got += n
+    def on_host(i: int) -> bool:   # FASTQ (or index=True): the host index
+        return index or fmt == N.KF_FMT_FASTQ or (fmt == N.KF_FMT_AUTO and sizes[i] > 0 and d[int(off[i])] == ord("@"))
 
     def host_index(i: int):
         lo, sz = int(off[i]), sizes[i]
-        d[lo + sz: int(off[i + 1])] = 10
-        if not index and fmt != N.KF_FMT_FASTQ and not (fmt == N.KF_FMT_AUTO and sz > 0 and d[lo] == ord("@")):
-            return None   # FASTA: the device indexes it
-        return index_records(d[lo: lo + sz], fmt, lo)[0]
+        return index_records(d[lo: lo + sz], fmt, lo)[0] if on_host(i) else None
 
-    try:
-        if pool is not None:
-            list(pool.map(read, tasks))
-            excl = list(pool.map(host_index, range(len(paths))))
-        elif threads > 1 and len(tasks) > 1:
-            with ThreadPoolExecutor(max_workers=min(threads, len(tasks))) as ex:
-                list(ex.map(read, tasks))
-                excl = list(ex.map(host_index, range(len(paths))))
-        else:
-            for t in tasks:
-                read(t)
-            excl = [host_index(i) for i in range(len(paths))]
-    finally:
-        for fd in fds:
-            os.close(fd)
+    if not any(on_host(i) for i in range(len(paths))):   # FASTA only: the device indexes it
+        return HostBatch(data, off, None, list(names) if names else list(paths))
+    if pool is not None:
+        excl = list(pool.map(host_index, range(len(paths))))
+    elif threads > 1 and len(paths) > 1:
+        with ThreadPoolExecutor(max_workers=min(threads, len(paths))) as ex:
+            excl = list(ex.map(host_index, range(len(paths))))
+    else:
+        excl = [host_index(i) for i in range(len(paths))]
     if not index and all(e is None for e in excl):
         return HostBatch(data, off, None, list(names) if names else list(paths))
     excl = [e if e is not None else index_records(d[int(off[i]): int(off[i]) + sizes[i]], N.KF_FMT_FASTA,

@@ -4,6 +4,7 @@
 #include <emmintrin.h>
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
@@ -413,6 +414,69 @@ uint64_t format_line(const char* name, const T* c, uint64_t nb, int pseudo, int 
     return (uint64_t)(p - out);
 }
 }  // namespace
+
+extern "C" int kf_read_files(const char* const* paths, int32_t n, const uint64_t* sizes, const uint64_t* off,
+                             uint8_t* dst, uint64_t piece, int n_threads) {
+    if (n < 0 || (n && (!paths || !sizes || !off || !dst))) return kf_fail(KF_EINVAL, "null argument");
+    if (n == 0) return KF_OK;
+    if (piece < 4096) piece = 4096;
+    if (n_threads < 1) n_threads = 1;
+    std::vector<int> fds((size_t)n, -1);
+    std::vector<uint64_t> first((size_t)n + 1, 0);   // first piece of each file
+    for (int32_t i = 0; i < n; ++i) {
+        if (off[i + 1] < off[i] + sizes[i]) return kf_fail(KF_EINVAL, "file %d does not fit its slot", i);
+        first[i + 1] = first[i] + (sizes[i] + piece - 1) / piece;
+    }
+    const uint64_t npiece = first[n];
+    std::atomic<uint64_t> next{0};
+    std::atomic<int> err{0};
+    std::string errmsg;
+    std::mutex mu;
+    auto fail = [&](const std::string& m) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!err.exchange(1)) errmsg = m;
+    };
+    for (int32_t i = 0; i < n; ++i) {   // open (and check the sizes) first: a missing file fails before any read
+        fds[i] = open(paths[i], O_RDONLY | O_CLOEXEC);
+        struct stat st;
+        if (fds[i] < 0 || fstat(fds[i], &st) != 0 || (uint64_t)st.st_size != sizes[i]) {
+            fail(std::string("cannot read ") + paths[i] + (fds[i] < 0 ? "" : " (size changed)"));
+            break;
+        }
+    }
+    auto work = [&]() {
+        for (;;) {
+            const uint64_t t = next.fetch_add(1);
+            if (t >= npiece || err.load()) break;
+            const int32_t i = (int32_t)(std::upper_bound(first.begin(), first.end(), t) - first.begin()) - 1;
+            const uint64_t a = (t - first[i]) * piece, e = std::min(sizes[i], a + piece);
+            uint64_t got = a;
+            while (got < e) {
+                const ssize_t r = pread(fds[i], dst + off[i] + got, e - got, (off_t)got);
+                if (r < 0 && errno == EINTR) continue;
+                if (r <= 0) {
+                    fail(std::string("short read on ") + paths[i]);
+                    return;
+                }
+                got += (uint64_t)r;
+            }
+            if (e == sizes[i]) memset(dst + off[i] + sizes[i], '\n', off[i + 1] - off[i] - sizes[i]);
+        }
+    };
+    if (!err.load()) {
+        const int nt = (int)std::min<uint64_t>((uint64_t)n_threads, npiece ? npiece : 1);
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+    }
+    for (int32_t i = 0; i < n; ++i)
+        if (fds[i] >= 0) close(fds[i]);
+    for (int32_t i = 0; i < n; ++i)   // empty files: their padding (no piece covers them)
+        if (sizes[i] == 0) memset(dst + off[i], '\n', off[i + 1] - off[i]);
+    if (err.load()) return kf_fail(KF_EINVAL, "%s", errmsg.c_str());
+    return KF_OK;
+}
 
 extern "C" int kf_format_kf(const char* name, const uint32_t* counts, uint64_t nbins, int pseudocount,
                             int raw_cnt, char* out, uint64_t cap, uint64_t* written) {

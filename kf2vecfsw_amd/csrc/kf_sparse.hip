@@ -42,6 +42,9 @@
 // gkeys[g] of them, bucket b from gbase[g][b].
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <cstdio>
 
 #include "kf_internal.h"
 
@@ -773,7 +776,8 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                                                             int bshift, const uint64_t* goff, uint32_t* flags,
                                                             uint64_t* cstatus, uint32_t* ticket,
                                                             const uint32_t* order, uint64_t* __restrict__ okeys,
-                                                            uint32_t* __restrict__ ocounts, uint64_t* unq) {
+                                                            uint32_t* __restrict__ ocounts, uint64_t* unq,
+                                                            unsigned long long* prof) {
     using CO = ChunkOf<KeyT>;
     constexpr int PER = CO::per;
     __shared__ uint32_t wc[kCWaves][128];   // packed u16 digit counters per wave; the head bit mask after the sort
@@ -782,6 +786,17 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
     extern __shared__ __attribute__((aligned(16))) uint8_t sp_dyn[];
     KeyT* stage = (KeyT*)sp_dyn;   // cap keys
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // KF_SPARSE_PROFILE (profiling builds): per-phase cycles of thread 0, added up
+    // per workgroup: load + first pass, second pass, run fix-up, head flags, look-back, stores
+    unsigned long long pt[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tmark = 0;
+    auto tick = [&](int ph) {
+        if (prof && tid == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (ph >= 0) pt[ph] += t - tmark;
+            tmark = t;
+        }
+    };
     for (;;) {
         if (tid == 0) {
             const uint32_t x = atomicAdd(ticket, 1u);
@@ -789,7 +804,12 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
         }
         __syncthreads();
         const uint32_t c = cid;
-        if (c >= cfirst[n]) return;   // uniform
+        if (c >= cfirst[n]) {   // uniform
+            if (prof && tid == 0)
+                for (int x = 0; x < 7; ++x) atomicAdd(&prof[x], pt[x]);
+            return;
+        }
+        tick(-1);
         const uint32_t g = cfirst[n + 2 + c];
         const Chunk ch = chunks[c];
         const uint32_t c0 = cfirst[g];
@@ -879,7 +899,10 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                     for (int it = 0; it < PER; ++it) srow[it * 64] = y[it];
                     __syncthreads();
                 }
-                for (int p = 0; p < np; ++p) pass(lo + 8 * p, p + 1 < np);
+                for (int p = 0; p < np; ++p) {
+                    pass(lo + 8 * p, p + 1 < np);
+                    tick(p == 0 ? 0 : 1);
+                }
                 if (!msd) break;
                 // run starts: bit i of hm (ballots over striped slots: consecutive lanes,
                 // consecutive slots, so the LDS reads do not conflict)
@@ -925,7 +948,9 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                         stage[j] = v;
                     }
                 }
-                if (!__syncthreads_or(lng)) break;
+                const bool again = __syncthreads_or(lng);
+                tick(2);
+                if (!again) break;
 #pragma unroll
                 for (int it = 0; it < PER; ++it) y[it] = srow[it * 64];
                 __syncthreads();
@@ -951,6 +976,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             }
             if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u);   // the sort's self-check
             __syncthreads();
+            tick(3);
             uint32_t nu;
             {
                 const uint32_t wd = hm[tid];   // 512 threads, one word each
@@ -962,6 +988,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 if (last) unq[g] = (uint64_t)bf + nu;
             }
             __syncthreads();
+            tick(4);
             const uint64_t o0 = obase + before_s;
 #pragma unroll 4
             for (int it = 0; it < PER; ++it) {
@@ -982,6 +1009,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 ocounts[o0 + j] = min(nx, nk) - i;
             }
             __syncthreads();   // stage, wc, cid are reused by the next chunk
+            tick(5);
         } else {
             // ------------------------------------------------ big bucket (sorted in the overflow area)
             const KeyT* x = ovf + ch.ovf;
@@ -1232,12 +1260,29 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
         corder = at32(L.corder);
         hipLaunchKernelGGL(sp_order_kernel, dim3(L.cmax / kSBlock + 1), dim3(kSBlock), 0, s, at32(L.cfirst), n, corder);
     }
+    unsigned long long* prof = nullptr;
+#ifdef KF_PROFILE_BUILD
+    const char* pe = getenv("KF_SPARSE_PROFILE");   // debugging aid: synchronous, prints to stderr
+    if (pe && *pe == '1' && (hipMalloc((void**)&prof, 64) != hipSuccess || hipMemsetAsync(prof, 0, 64, s) != hipSuccess))
+        return kf_fail(KF_EHIP, "profile buffer");
+#endif
     hipLaunchKernelGGL(sp2_chunk_kernel<KeyT>, dim3((uint32_t)cus), dim3(kCBlock), ChunkOf<KeyT>::cap * sizeof(KeyT), s,
                        kb, ovf, (const Chunk*)(work + L.chunks), at32(L.cfirst), n, B, d_goff, &tfirst[n + 1],
                        (uint64_t*)(work + L.cstatus), at32(L.cticket), corder, d_keys, d_counts,
-                       (uint64_t*)(work + L.unq));
+                       (uint64_t*)(work + L.unq), prof);
     // the overflow sort's flag word (look-back stall) when it ran, else the main one
     const uint32_t* oflags = passes > 0 ? at32(L.otfirst) + L.smax + 1 : &tfirst[n + 1];
+#ifdef KF_PROFILE_BUILD
+    if (prof) {
+        unsigned long long h[8] = {0};
+        if (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(h, prof, 56, hipMemcpyDeviceToHost) != hipSuccess)
+            return kf_fail(KF_EHIP, "profile readback");
+        (void)hipFree(prof);
+        fprintf(stderr, "[kf_sparse k=%d] chunk kernel, cycles summed over workgroups (thread 0): pass0+load %.3g "
+                "pass1 %.3g fixup %.3g heads %.3g lookback %.3g stores %.3g\n", k, (double)h[0], (double)h[1],
+                (double)h[2], (double)h[3], (double)h[4], (double)h[5]);
+    }
+#endif
     hipLaunchKernelGGL(sp2_final_kernel, dim3((n + 255) / 256), dim3(256), 0, s, tfirst, n, oflags,
                        (const uint64_t*)(work + L.unq), d_nuniq);
     return KF_OK;

@@ -374,3 +374,33 @@ def test_pack_files_without_index(native, tmp_path):
     mixed = C.pack_files([str(fa), str(fq), str(fb)], pin=False, threads=1, index=False)
     ref = C.pack_files([str(fa), str(fq), str(fb)], pin=False, threads=1)
     assert mixed.excl is not None and np.array_equal(mixed.excl, ref.excl)
+
+
+def test_read_files_pieces_padding_and_errors(native, tmp_path):
+    """kf_read_files (the CLI readers' native path): every file lands at its slot
+    whatever the piece size (pieces smaller than a file, files smaller than a
+    piece, empty files), the slot tails are '\\n', and a file that changed size
+    since it was stat'ed fails loudly naming it."""
+    import ctypes
+    import gen
+    from kf2vecfsw_amd import _native as N
+    from kf2vecfsw_amd import counter as C
+    rng = np.random.default_rng(44)
+    blobs = [gen.random_fasta(rng, int(rng.integers(0, 200000))) for _ in range(9)] + [b"", b">x\nAC\n"]
+    paths = []
+    for i, b in enumerate(blobs):
+        p = tmp_path / f"g{i}.fna"
+        p.write_bytes(b)
+        paths.append(str(p))
+    ref = C.pack_genomes(blobs, pin=False)
+    for piece, threads in ((4096, 1), (4096, 8), (1 << 16, 3), (1 << 30, 8)):
+        hb = C.pack_files(paths, pin=False, threads=threads, piece=piece, index=True)
+        assert np.array_equal(hb.data.numpy()[: int(hb.off[-1])], ref.data.numpy()[: int(ref.off[-1])])
+        assert np.array_equal(hb.excl, ref.excl)
+    sizes = np.array([len(b) for b in blobs], np.uint64)
+    off = C._layout(list(sizes))
+    dst = np.zeros(int(off[-1]), np.uint8)
+    sizes[3] += 1   # stale size
+    enc = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+    rc = native.kf_read_files(enc, len(paths), sizes.ctypes.data, off.ctypes.data, dst.ctypes.data, 4096, 4)
+    assert rc == N.KF_EINVAL and b"g3.fna" in native.kf_last_error()

@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--genomes", type=int, default=64)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default="/dev/shm/kf_e2e" if os.access("/dev/shm", os.W_OK) else "/tmp/kf_e2e")
-    ap.add_argument("--modes", default="read,register", help="KF_READ_MODE values to A/B in one process")
+    ap.add_argument("--modes", default="read", help="KF_READ_MODE values to A/B in one process (read, register)")
     ap.add_argument("--k", type=int, default=7)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
