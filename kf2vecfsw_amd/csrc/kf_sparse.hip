@@ -761,15 +761,23 @@ __device__ __forceinline__ uint32_t ceil_log2(uint32_t x) { return x <= 1 ? 0u :
 
 // ---- C2. chunk sort + run-length encoding (persistent, one 512-thread
 // workgroup per CU).  A chunk's keys (minus its first bucket's base: R = B +
-// ceil(log2 nb) bits) are sorted in LDS by stable LSD passes of 8 bits: per
-// pass a returning packed-u16 LDS add per key into its wave's digit counter
-// (stable: an LDS unit serves one instruction's lanes in lane order, and keys
-// are striped so lane, then iteration, then wave is slot order), one wave scans
-// the 256 x 16 counters, the keys go to their slots in LDS and come back
-// striped.  Then each thread takes `per` consecutive sorted keys: head flags
-// (a key unlike its predecessor) into an LDS bit mask, a block scan numbers the
-// heads, the chunk learns the genome's distinct k-mers before it by look-back,
-// and every head writes (key, distance to the next head).
+// ceil(log2 nb) bits) are loaded striped, 32 per thread, and sorted in LDS by
+// stable 8-bit passes: per pass a returning packed-u16 LDS add per key into its
+// wave's digit counter (stable: an LDS unit serves one instruction's lanes in
+// lane order, and keys are striped so lane, then iteration, then wave is slot
+// order), one wave turns the 256 x 8 counters into slots, the keys go to their
+// slots and come back striped.  For R > 16 only the top 16 bits are sorted that
+// way (two passes): a chunk of <= 16,384 keys over 65,536 values of those bits
+// leaves runs of a few keys with equal top bits, each sorted by the thread
+// owning the mask word of its start (insertion sort in LDS); a run longer than
+// kRun whose keys are not all equal (repeats make long runs of EQUAL keys, which
+// need nothing) sends the chunk through every pass (LSD takes any order).  One
+// striped sweep sets the run-start and head bits (a key unlike its predecessor)
+// in LDS masks; a block scan over the head words numbers the heads; the chunk
+// learns the genome's distinct k-mers before it by look-back, and every head
+// writes (key, distance to the next head), consecutive lanes at consecutive
+// outputs.  The next chunk's keys are loaded into the (dead) key registers as
+// soon as a chunk is sorted, so their latency hides behind the encoding.
 template <typename KeyT>
 __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restrict__ kb, const KeyT* __restrict__ ovf,
                                                             const Chunk* chunks, const uint32_t* cfirst, int n,
@@ -780,14 +788,20 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                                                             unsigned long long* prof) {
     using CO = ChunkOf<KeyT>;
     constexpr int PER = CO::per;
-    __shared__ uint32_t wc[kCWaves][128];   // packed u16 digit counters per wave; the head bit mask after the sort
+    constexpr uint32_t kWords = CO::cap / 32;   // mask words of a chunk
+    static_assert(kWords == (uint32_t)kCBlock && kCWaves * 128 >= 2 * kWords, "one mask word per thread");
+    __shared__ uint32_t wc[kCWaves][128];   // packed u16 digit counters per wave; after the sort: start | head masks
+    __shared__ uint32_t wpre[kWords];       // heads before each head-mask word
     __shared__ uint32_t wsum[kCWaves];
     __shared__ uint32_t cid, before_s;
     extern __shared__ __attribute__((aligned(16))) uint8_t sp_dyn[];
     KeyT* stage = (KeyT*)sp_dyn;   // cap keys
+    uint32_t* hs = &wc[0][0];          // run starts (top bits differ), kWords words
+    uint32_t* hh = &wc[0][0] + kWords; // heads (keys differ)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     // KF_SPARSE_PROFILE (profiling builds): per-phase cycles of thread 0, added up
-    // per workgroup: load + first pass, second pass, run fix-up, head flags, look-back, stores
+    // per workgroup: first pass (+ waits on the keys), second pass, masks + fix-up,
+    // head count, look-back, stores
     unsigned long long pt[7] = {0, 0, 0, 0, 0, 0, 0};
     unsigned long long tmark = 0;
     auto tick = [&](int ph) {
@@ -797,41 +811,30 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             tmark = t;
         }
     };
+    const uint32_t total = cfirst[n];
+    uint32_t li0 = (uint32_t)w * CO::wave_span + (uint32_t)lane;   // striped slot li0 + 64 it
+    KeyT* srow = stage + li0;
+    KeyT y[PER];
+    uint32_t rk[PER];
+    uint32_t c = 0xFFFFFFFFu;   // the chunk being worked on (none before the first ticket)
+    Chunk ch;
+    ch.ovf = kNoOvf;
     for (;;) {
-        if (tid == 0) {
-            const uint32_t x = atomicAdd(ticket, 1u);
-            cid = order && x < cfirst[n] ? order[x] : x;
+        const bool have = c < total;
+        uint32_t g = 0, c0 = 0, nk = 0;
+        bool last = false;
+        KeyT base = 0;
+        if (have) {
+            tick(-1);
+            g = cfirst[n + 2 + c];
+            c0 = cfirst[g];
+            last = c + 1 == cfirst[g + 1];
+            nk = ch.nkeys;
+            base = (KeyT)ch.blo << bshift;
         }
-        __syncthreads();
-        const uint32_t c = cid;
-        if (c >= cfirst[n]) {   // uniform
-            if (prof && tid == 0)
-                for (int x = 0; x < 7; ++x) atomicAdd(&prof[x], pt[x]);
-            return;
-        }
-        tick(-1);
-        const uint32_t g = cfirst[n + 2 + c];
-        const Chunk ch = chunks[c];
-        const uint32_t c0 = cfirst[g];
-        const bool last = c + 1 == cfirst[g + 1];
-        const uint64_t obase = goff[g];
-        const uint32_t nk = ch.nkeys;
-        if (ch.ovf == kNoOvf) {
-            // ------------------------------------------------ in-LDS sort
-            const KeyT base = (KeyT)ch.blo << bshift;
+        if (have && ch.ovf == kNoOvf) {
+            // ------------------------------------------------ in-LDS sort (y loaded)
             const uint32_t R = (uint32_t)bshift + ceil_log2(ch.nb);
-            // striped slot li0 + 64 it; `rem` keeps the 32 bounds tests from holding 32 slot registers
-            uint32_t li0 = (uint32_t)w * CO::wave_span + (uint32_t)lane;
-            asm volatile("" : "+v"(li0));   // per chunk: nothing derived from it is hoisted out of the loop
-            const int rem = (int)nk - (int)li0;
-            const KeyT* src = kb + ch.start + li0;
-            KeyT* srow = stage + li0;
-            KeyT y[PER];
-            uint32_t rk[PER];
-#pragma unroll
-            for (int it = 0; it < PER; ++it)   // padding sorts last (all ones below R bits and above)
-                y[it] = it * 64 < rem ? (KeyT)(src[it * 64] - base) : (KeyT)~(KeyT)0;
-            // one stable pass by the 8-bit digit at bit sh8: keys y (striped) -> stage in digit order
             auto pass = [&](int sh8, bool reload) __attribute__((always_inline)) {
                 for (int i = tid; i < kCWaves * 128; i += kCBlock) (&wc[0][0])[i] = 0;
                 __syncthreads();
@@ -882,13 +885,6 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                     for (int it = 0; it < PER; ++it) y[it] = srow[it * 64];
                 }
             };
-            // Round 0: for R > 16 the most significant 16 bits only (two passes): a chunk
-            // holds <= 16,384 keys over 65,536 values of those bits, so what is left
-            // unsorted is runs of a few keys with equal top bits, each sorted by one
-            // thread in LDS.  A run longer than kRun whose keys are not all equal
-            // (repeats make long runs of EQUAL keys, which need nothing) sends the chunk
-            // to round 1: every bit below R, least significant digit first (LSD sorts
-            // any order).  For R <= 16 round 0 is that full LSD.
             constexpr uint32_t kRun = 32;
             for (int round = 0; round < 2; ++round) {
                 const bool msd = round == 0 && R > 16;
@@ -903,49 +899,64 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                     pass(lo + 8 * p, p + 1 < np);
                     tick(p == 0 ? 0 : 1);
                 }
-                if (!msd) break;
-                // run starts: bit i of hm (ballots over striped slots: consecutive lanes,
-                // consecutive slots, so the LDS reads do not conflict)
-                uint32_t* hm = &wc[0][0];   // 512 words = slots 0 .. 16,383
-                static_assert(CO::cap == 32 * 512 && kCWaves * 128 >= 1024, "head mask + word prefix fit wc");
+                // one striped sweep: run starts (the top bits above `lo` differ) and heads
+                // (the keys differ); the order check on the sorted bits (every key is in
+                // order when lo = 0).  Consecutive lanes read consecutive slots.
+                bool disorder = false;
 #pragma unroll 4
                 for (int it = 0; it < PER; ++it) {
                     const uint32_t i = li0 + (uint32_t)it * 64;
-                    const KeyT v = srow[it * 64] >> lo, pv = i ? stage[i - 1] >> lo : (KeyT)0;
-                    const uint64_t b64 = __ballot(i < nk && (i == 0 || v != pv));
+                    const KeyT v = srow[it * 64], pv = i ? stage[i - 1] : (KeyT)0;
+                    const bool in = i < nk, lead = i == 0;
+                    disorder |= in && !lead && (v >> lo) < (pv >> lo);
+                    const uint64_t bs = __ballot(in && (lead || (v >> lo) != (pv >> lo)));
+                    const uint64_t bh = __ballot(in && (lead || v != pv));
                     if (lane == 0) {
-                        hm[i >> 5] = (uint32_t)b64;
-                        hm[(i >> 5) + 1] = (uint32_t)(b64 >> 32);
+                        hs[i >> 5] = (uint32_t)bs;
+                        hs[(i >> 5) + 1] = (uint32_t)(bs >> 32);
+                        hh[i >> 5] = (uint32_t)bh;
+                        hh[(i >> 5) + 1] = (uint32_t)(bh >> 32);
                     }
                 }
+                if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u);   // the sort's self-check
                 __syncthreads();
+                if (!msd) break;
+                // runs of two or more keys start where a start bit is followed by a clear
+                // one: rare; the thread owning the start's word sorts the run and
+                // recomputes the head bits inside it
                 bool lng = false;
-#pragma unroll 4
-                for (int it = 0; it < PER; ++it) {
-                    const uint32_t st = li0 + (uint32_t)it * 64;
-                    if (st >= nk || !((hm[st >> 5] >> (st & 31u)) & 1u)) continue;
-                    uint32_t en = nk;   // the next run start (bits past nk are 0)
-                    for (uint32_t pos = st + 1; pos < nk; pos = (pos | 31u) + 1u) {
-                        const uint32_t wd = hm[pos >> 5] >> (pos & 31u);
-                        if (wd) {
-                            en = pos + (uint32_t)__builtin_ctz(wd);
-                            break;
+                {
+                    const uint32_t m = hs[tid], nb0 = tid + 1 < (int)kWords ? hs[tid + 1] & 1u : 0u;
+                    for (uint32_t cand = m & ~((m >> 1) | (nb0 << 31)); cand; cand &= cand - 1u) {
+                        const uint32_t st = 32u * (uint32_t)tid + (uint32_t)__builtin_ctz(cand);
+                        uint32_t en = nk;   // the next run start (bits past nk are 0)
+                        for (uint32_t pos = st + 1; pos < nk; pos = (pos | 31u) + 1u) {
+                            const uint32_t wd = hs[pos >> 5] >> (pos & 31u);
+                            if (wd) {
+                                en = pos + (uint32_t)__builtin_ctz(wd);
+                                break;
+                            }
                         }
-                    }
-                    if (en - st < 2) continue;
-                    if (en - st > kRun) {   // long: fine only if every key equals the first
-                        const KeyT f = stage[st];
-                        for (uint32_t i = st + 1; i < en && !lng; ++i) lng = stage[i] != f;
-                        continue;
-                    }
-                    for (uint32_t i = st + 1; i < en; ++i) {   // insertion sort (stable)
-                        const KeyT v = stage[i];
-                        uint32_t j = i;
-                        while (j > st && stage[j - 1] > v) {
-                            stage[j] = stage[j - 1];
-                            --j;
+                        if (st >= nk || en - st < 2) continue;
+                        if (en - st > kRun) {   // long: fine only if every key equals the first
+                            const KeyT f = stage[st];
+                            for (uint32_t i = st + 1; i < en && !lng; ++i) lng = stage[i] != f;
+                            continue;
                         }
-                        stage[j] = v;
+                        for (uint32_t i = st + 1; i < en; ++i) {   // insertion sort
+                            const KeyT v = stage[i];
+                            uint32_t j = i;
+                            while (j > st && stage[j - 1] > v) {
+                                stage[j] = stage[j - 1];
+                                --j;
+                            }
+                            stage[j] = v;
+                        }
+                        for (uint32_t i = st + 1; i < en; ++i) {   // the run's head bits, in order now
+                            const uint32_t bit = 1u << (i & 31u);
+                            if (stage[i] != stage[i - 1]) atomicOr(&hh[i >> 5], bit);
+                            else atomicAnd(&hh[i >> 5], ~bit);
+                        }
                     }
                 }
                 const bool again = __syncthreads_or(lng);
@@ -955,33 +966,34 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 for (int it = 0; it < PER; ++it) y[it] = srow[it * 64];
                 __syncthreads();
             }
-            __syncthreads();
+        }
+        // ---------------------------------------------------- next chunk: its keys into y now
+        if (tid == 0) {
+            const uint32_t x = atomicAdd(ticket, 1u);
+            cid = order && x < total ? order[x] : x;
+        }
+        __syncthreads();
+        const uint32_t cn = cid;
+        Chunk chn;
+        chn.ovf = kNoOvf;
+        if (cn < total) {
+            chn = chunks[cn];
+            if (chn.ovf == kNoOvf) {
+                uint32_t l = li0;
+                asm volatile("" : "+v"(l));   // per chunk: nothing derived from it is hoisted out of the loop
+                const int rem = (int)chn.nkeys - (int)l;
+                const KeyT* src = kb + chn.start + l;
+                const KeyT bn = (KeyT)chn.blo << bshift;
+#pragma unroll
+                for (int it = 0; it < PER; ++it)   // padding sorts last (all ones below R bits and above)
+                    y[it] = it * 64 < rem ? (KeyT)(src[it * 64] - bn) : (KeyT)~(KeyT)0;
+            }
+        }
+        if (have && ch.ovf == kNoOvf) {
             // ------------------------------------------------ run-length encoding
-            // Striped again: head bit i = a key unlike its predecessor (ballots); word
-            // prefix counts number the heads; consecutive lanes hold consecutive slots,
-            // so the (key, count) stores of a wave are contiguous.
-            uint32_t* hm = &wc[0][0];        // head bits, 512 words
-            uint32_t* wpre = &wc[0][0] + 512;   // heads before each word
-            bool disorder = false;
-#pragma unroll 4
-            for (int it = 0; it < PER; ++it) {
-                const uint32_t i = li0 + (uint32_t)it * 64;
-                const KeyT v = srow[it * 64], pv = i ? stage[i - 1] : (KeyT)0;
-                disorder |= i < nk && i > 0 && v < pv;
-                const uint64_t b64 = __ballot(i < nk && (i == 0 || v != pv));
-                if (lane == 0) {
-                    hm[i >> 5] = (uint32_t)b64;
-                    hm[(i >> 5) + 1] = (uint32_t)(b64 >> 32);
-                }
-            }
-            if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u);   // the sort's self-check
-            __syncthreads();
-            tick(3);
             uint32_t nu;
-            {
-                const uint32_t wd = hm[tid];   // 512 threads, one word each
-                wpre[tid] = block_excl_scan<kCWaves>((uint32_t)__builtin_popcount(wd), wsum, &nu);
-            }
+            wpre[tid] = block_excl_scan<kCWaves>((uint32_t)__builtin_popcount(hh[tid]), wsum, &nu);
+            tick(3);
             if (tid == 0) {
                 const uint32_t bf = lookback(cstatus, 1, flags, c, c0, nu, 1u);
                 before_s = bf;
@@ -989,17 +1001,17 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             }
             __syncthreads();
             tick(4);
-            const uint64_t o0 = obase + before_s;
+            const uint64_t o0 = goff[g] + before_s;
 #pragma unroll 4
             for (int it = 0; it < PER; ++it) {
                 const uint32_t i = li0 + (uint32_t)it * 64;
                 if (i >= nk) continue;
-                const uint32_t wd = hm[i >> 5];
+                const uint32_t wd = hh[i >> 5];
                 if (!((wd >> (i & 31u)) & 1u)) continue;
                 const uint32_t j = wpre[i >> 5] + (uint32_t)__builtin_popcount(wd & ((1u << (i & 31u)) - 1u));
                 uint32_t nx = nk;
                 for (uint32_t pos = i + 1; pos < nk; pos = (pos | 31u) + 1u) {
-                    const uint32_t w2 = hm[pos >> 5] >> (pos & 31u);
+                    const uint32_t w2 = hh[pos >> 5] >> (pos & 31u);
                     if (w2) {
                         nx = pos + (uint32_t)__builtin_ctz(w2);
                         break;
@@ -1008,9 +1020,9 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 okeys[o0 + j] = (uint64_t)(srow[it * 64] + base);
                 ocounts[o0 + j] = min(nx, nk) - i;
             }
-            __syncthreads();   // stage, wc, cid are reused by the next chunk
+            __syncthreads();   // stage, masks, cid are reused by the next chunk
             tick(5);
-        } else {
+        } else if (have) {
             // ------------------------------------------------ big bucket (sorted in the overflow area)
             const KeyT* x = ovf + ch.ovf;
             uint32_t cnt = 0;
@@ -1029,7 +1041,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 if (last) unq[g] = (uint64_t)bf + nu;
             }
             __syncthreads();
-            const uint64_t o0 = obase + before_s;
+            const uint64_t o0 = goff[g] + before_s;
             // heads in order: key and (temporarily) its slot
             uint32_t run = 0;
             for (uint32_t r = 0; r < nk; r += kCBlock) {
@@ -1061,6 +1073,13 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 __syncthreads();
             }
         }
+        if (cn >= total) {
+            if (prof && tid == 0)
+                for (int x = 0; x < 7; ++x) atomicAdd(&prof[x], pt[x]);
+            return;
+        }
+        c = cn;
+        ch = chn;
     }
 }
 

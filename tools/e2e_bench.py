@@ -52,7 +52,8 @@ def main():
     ap.add_argument("--genomes", type=int, default=64)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default="/dev/shm/kf_e2e" if os.access("/dev/shm", os.W_OK) else "/tmp/kf_e2e")
-    ap.add_argument("--modes", default="read", help="KF_READ_MODE values to A/B in one process (read, register)")
+    ap.add_argument("--modes", default="read", help="variants to A/B in one process: name[:ENV=VAL[+ENV=VAL]],... "
+                    "(name read/register also sets KF_READ_MODE)")
     ap.add_argument("--k", type=int, default=7)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
@@ -80,24 +81,40 @@ def main():
     # A/B in one process: each read mode pipelined (auto batch size), and one batch
     import contextlib
     import io
-    modes = [m for m in args.modes.split(",") if m]
+    variants = {}
+    for spec in [m for m in args.modes.split(",") if m]:
+        name, _, envs = spec.partition(":")
+        env = dict(kv.split("=", 1) for kv in envs.split("+") if kv)
+        if name in ("read", "register"):
+            env.setdefault("KF_READ_MODE", name)
+        variants[name] = env
+    modes = list(variants)
+    base_env = {k: os.environ.get(k) for e in variants.values() for k in e}
+
+    def set_env(m):
+        for k, v in base_env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        os.environ.update(variants[m])
     walls = {m: [] for m in modes}
     walls["one_batch"] = []
     parity_modes = {}
     for _ in range(args.reps):
         for m in modes:
-            os.environ["KF_READ_MODE"] = m
+            set_env(m)
             t0 = time.perf_counter()
             with contextlib.redirect_stdout(io.StringIO()):
                 M.main(cli)
             walls[m].append(time.perf_counter() - t0)
-        os.environ["KF_READ_MODE"] = "read"
+        set_env(modes[0])
         t0 = time.perf_counter()
         with contextlib.redirect_stdout(io.StringIO()):
             M.main(cli + ["-batch_gb", "64"])
         walls["one_batch"].append(time.perf_counter() - t0)
     for m in modes:   # each mode's files against the oracle (below: the last run's)
-        os.environ["KF_READ_MODE"] = m
+        set_env(m)
         o2 = out + "_" + m
         os.makedirs(o2, exist_ok=True)
         with contextlib.redirect_stdout(io.StringIO()):
@@ -109,12 +126,12 @@ def main():
     for m in modes:
         buf = io.StringIO()
         os.environ["KF_TRACE"] = "1"
-        os.environ["KF_READ_MODE"] = m
+        set_env(m)
         with contextlib.redirect_stderr(buf), contextlib.redirect_stdout(io.StringIO()):
             M.main(cli)
         del os.environ["KF_TRACE"]
         trace[m] = [json.loads(line) for line in buf.getvalue().splitlines() if line.startswith('{"kf_trace"')]
-    os.environ["KF_READ_MODE"] = "read"
+    set_env(modes[0])
 
     # phase breakdown on the same files
     dev = torch.device("cuda:0")
