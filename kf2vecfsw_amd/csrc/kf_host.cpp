@@ -17,6 +17,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -415,6 +417,100 @@ uint64_t format_line(const char* name, const T* c, uint64_t nb, int pseudo, int 
 }
 }  // namespace
 
+// ------------------------------------------------------------------ host worker pool
+// One process-wide pool of native worker threads for the host-side batch work
+// (file reads, .kf formatting): a call submits n independent items and takes part
+// itself; no threads are created per call, and concurrent calls (the CLI reads
+// the next batches while the writer formats the last one) share the workers
+// instead of oversubscribing the CPUs.
+namespace {
+struct PoolJob {
+    std::function<void(uint64_t)> fn;
+    uint64_t n = 0;
+    int max_helpers = 0;                 // pool workers allowed on this job
+    std::atomic<uint64_t> next{0}, done{0};
+    std::atomic<int> helpers{0};
+    std::mutex mu;
+    std::condition_variable cv;
+};
+struct HostPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::shared_ptr<PoolJob>> jobs;
+    std::vector<std::thread> th;
+    void ensure(int n) {   // caller holds mu
+        while ((int)th.size() < n) th.emplace_back([this] { loop(); });
+    }
+    void loop() {
+        for (;;) {
+            std::shared_ptr<PoolJob> j;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !jobs.empty(); });
+                for (auto& x : jobs)
+                    if (x->next.load() < x->n && x->helpers.load() < x->max_helpers) {
+                        j = x;
+                        break;
+                    }
+                if (!j) {   // every queued job is fully handed out: wait for a new one
+                    cv.wait(lk);
+                    continue;
+                }
+                j->helpers.fetch_add(1);
+            }
+            run(*j);
+            j->helpers.fetch_sub(1);
+        }
+    }
+    static void run(PoolJob& j) {
+        for (;;) {
+            const uint64_t t = j.next.fetch_add(1);
+            if (t >= j.n) return;
+            j.fn(t);
+            if (j.done.fetch_add(1) + 1 == j.n) {
+                std::lock_guard<std::mutex> lk(j.mu);
+                j.cv.notify_all();
+            }
+        }
+    }
+};
+HostPool& host_pool() {
+    static HostPool* p = new HostPool;   // never destroyed: workers outlive static teardown
+    return *p;
+}
+}  // namespace
+
+// Runs fn(0..n-1) on up to n_threads threads (the caller plus pool workers).
+static void host_parallel(uint64_t n, int n_threads, const std::function<void(uint64_t)>& fn) {
+    if (n == 0) return;
+    if (n_threads <= 1 || n == 1) {
+        for (uint64_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    auto j = std::make_shared<PoolJob>();
+    j->fn = fn;
+    j->n = n;
+    j->max_helpers = (int)std::min<uint64_t>((uint64_t)n_threads - 1, n - 1);
+    HostPool& P = host_pool();
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        P.ensure(std::min(n_threads - 1, 255));
+        P.jobs.push_back(j);
+    }
+    P.cv.notify_all();
+    HostPool::run(*j);
+    {
+        std::unique_lock<std::mutex> lk(j->mu);
+        j->cv.wait(lk, [&] { return j->done.load() == j->n; });
+    }
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (auto it = P.jobs.begin(); it != P.jobs.end(); ++it)
+        if (*it == j) {
+            P.jobs.erase(it);
+            break;
+        }
+}
+
 extern "C" int kf_read_files(const char* const* paths, int32_t n, const uint64_t* sizes, const uint64_t* off,
                              uint8_t* dst, uint64_t piece, int n_threads) {
     if (n < 0 || (n && (!paths || !sizes || !off || !dst))) return kf_fail(KF_EINVAL, "null argument");
@@ -428,7 +524,6 @@ extern "C" int kf_read_files(const char* const* paths, int32_t n, const uint64_t
         first[i + 1] = first[i] + (sizes[i] + piece - 1) / piece;
     }
     const uint64_t npiece = first[n];
-    std::atomic<uint64_t> next{0};
     std::atomic<int> err{0};
     std::string errmsg;
     std::mutex mu;
@@ -444,10 +539,9 @@ extern "C" int kf_read_files(const char* const* paths, int32_t n, const uint64_t
             break;
         }
     }
-    auto work = [&]() {
-        for (;;) {
-            const uint64_t t = next.fetch_add(1);
-            if (t >= npiece || err.load()) break;
+    auto piece_fn = [&](uint64_t t) {
+        {
+            if (err.load()) return;
             const int32_t i = (int32_t)(std::upper_bound(first.begin(), first.end(), t) - first.begin()) - 1;
             const uint64_t a = (t - first[i]) * piece, e = std::min(sizes[i], a + piece);
             uint64_t got = a;
@@ -463,13 +557,7 @@ extern "C" int kf_read_files(const char* const* paths, int32_t n, const uint64_t
             if (e == sizes[i]) memset(dst + off[i] + sizes[i], '\n', off[i + 1] - off[i] - sizes[i]);
         }
     };
-    if (!err.load()) {
-        const int nt = (int)std::min<uint64_t>((uint64_t)n_threads, npiece ? npiece : 1);
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(work);
-        work();
-        for (auto& t : th) t.join();
-    }
+    if (!err.load()) host_parallel(npiece, n_threads, piece_fn);
     for (int32_t i = 0; i < n; ++i)
         if (fds[i] >= 0) close(fds[i]);
     for (int32_t i = 0; i < n; ++i)   // empty files: their padding (no piece covers them)
@@ -494,38 +582,30 @@ extern "C" int kf_format_kf(const char* name, const uint32_t* counts, uint64_t n
 extern "C" int kf_write_kf_files(const char* dir, const char* const* names, int32_t n, const uint32_t* counts,
                                  uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
     if (!dir || (!names && n) || (!counts && n)) return kf_fail(KF_EINVAL, "null argument");
-    if (n_threads < 1) n_threads = 1;
-    n_threads = std::min<int>(n_threads, std::max<int32_t>(n, 1));
-    std::atomic<int32_t> next{0};
+    if (n <= 0) return KF_OK;
     std::atomic<int> err{0};
     std::string errmsg;
     std::mutex mu;
-    auto work = [&]() {
-        std::vector<char> buf;
-        std::string path;
-        for (;;) {
-            const int32_t i = next.fetch_add(1);
-            if (i >= n || err.load()) break;
-            buf.resize(kf_line_cap(strlen(names[i]), nbins));
-            const uint64_t w = format_line(names[i], counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt,
-                                           buf.data());
-            path.assign(dir);
-            path += "/";
-            path += names[i];
-            path += ".kf";
-            FILE* f = fopen(path.c_str(), "wb");
-            bool ok = f && fwrite(buf.data(), 1, w, f) == w;
-            if (f) ok = (fclose(f) == 0) && ok;
-            if (!ok) {
-                std::lock_guard<std::mutex> lk(mu);
-                if (!err.exchange(1)) errmsg = "cannot write " + path;
-            }
+    host_parallel((uint64_t)n, std::max(1, n_threads), [&](uint64_t gi) {
+        const int32_t i = (int32_t)gi;
+        if (err.load()) return;
+        thread_local std::vector<char> buf;   // per worker, kept across calls
+        thread_local std::string path;
+        buf.resize(kf_line_cap(strlen(names[i]), nbins));
+        const uint64_t w = format_line(names[i], counts + (uint64_t)i * nbins, nbins, pseudocount, raw_cnt,
+                                       buf.data());
+        path.assign(dir);
+        path += "/";
+        path += names[i];
+        path += ".kf";
+        FILE* f = fopen(path.c_str(), "wb");
+        bool ok = f && fwrite(buf.data(), 1, w, f) == w;
+        if (f) ok = (fclose(f) == 0) && ok;
+        if (!ok) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err.exchange(1)) errmsg = "cannot write " + path;
         }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < n_threads; ++t) th.emplace_back(work);
-    work();
-    for (auto& t : th) t.join();
+    });
     if (err.load()) return kf_fail(KF_EINVAL, "%s", errmsg.c_str());
     return KF_OK;
 }

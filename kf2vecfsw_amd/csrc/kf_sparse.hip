@@ -129,9 +129,14 @@ __device__ __forceinline__ bool tile_span(const uint64_t* goff, const uint32_t* 
     return true;
 }
 
+// Barrier for LDS traffic only: outstanding global loads and stores stay in
+// flight across it (__syncthreads() is a workgroup fence too, which waits for
+// every outstanding global access of the wave first).
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Exclusive prefix of one value per thread over an NW-wave workgroup; *total
-// (optional) gets the sum.  Contains two barriers.
-template <int NW>
+// (optional) gets the sum.  Contains two barriers (LDS-only ones if LDSB).
+template <int NW, bool LDSB = false>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total = nullptr) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t inc = v;
@@ -140,7 +145,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
         if (lane >= d) inc += o;
     }
     if (lane == 63) wsum[w] = inc;
-    __syncthreads();
+    if (LDSB) lds_sync();
+    else __syncthreads();
     uint32_t before = 0, all = 0;
 #pragma unroll
     for (int x = 0; x < NW; ++x) {
@@ -149,7 +155,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
         all += s;
     }
     if (total) *total = all;
-    __syncthreads();
+    if (LDSB) lds_sync();
+    else __syncthreads();
     return before + inc - v;
 }
 
@@ -972,7 +979,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             const uint32_t x = atomicAdd(ticket, 1u);
             cid = order && x < total ? order[x] : x;
         }
-        __syncthreads();
+        __syncthreads();   // (nothing of this chunk is in flight yet)
         const uint32_t cn = cid;
         Chunk chn;
         chn.ovf = kNoOvf;
@@ -991,15 +998,16 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
         }
         if (have && ch.ovf == kNoOvf) {
             // ------------------------------------------------ run-length encoding
+            // (LDS-only barriers from here on: the next chunk's key loads stay in flight)
             uint32_t nu;
-            wpre[tid] = block_excl_scan<kCWaves>((uint32_t)__builtin_popcount(hh[tid]), wsum, &nu);
+            wpre[tid] = block_excl_scan<kCWaves, true>((uint32_t)__builtin_popcount(hh[tid]), wsum, &nu);
             tick(3);
             if (tid == 0) {
                 const uint32_t bf = lookback(cstatus, 1, flags, c, c0, nu, 1u);
                 before_s = bf;
                 if (last) unq[g] = (uint64_t)bf + nu;
             }
-            __syncthreads();
+            lds_sync();
             tick(4);
             const uint64_t o0 = goff[g] + before_s;
 #pragma unroll 4
@@ -1020,7 +1028,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 okeys[o0 + j] = (uint64_t)(srow[it * 64] + base);
                 ocounts[o0 + j] = min(nx, nk) - i;
             }
-            __syncthreads();   // stage, masks, cid are reused by the next chunk
+            lds_sync();   // stage, masks, cid are reused by the next chunk
             tick(5);
         } else if (have) {
             // ------------------------------------------------ big bucket (sorted in the overflow area)
