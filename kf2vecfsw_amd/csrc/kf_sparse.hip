@@ -588,7 +588,7 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
             const uint32_t x = atomicAdd(ticket, 1u);
             tix = order && x < tfirst[n] ? order[x] : x;
         }
-        __syncthreads();
+        lds_sync();
         const uint32_t t = tix;
         TileSpan ts;
         if (!tile_span(goff, tfirst, n, t, ts, kTB)) return;   // uniform: no tiles left
@@ -597,14 +597,14 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
         for (int j = 0; j < kEB; ++j) key[j] = sent;
         emit_row(bytes, ts, t, n_excl, excl, xlo, k, key);
         for (int i = tid; i < kBWaves * (int)kNB / 2; i += kBBlock) (&wc[0][0])[i] = 0;
-        __syncthreads();
+        lds_sync();
         uint32_t rk[kEB];
 #pragma unroll
         for (int j = 0; j < kEB; ++j) {
             const uint32_t b = (uint32_t)(key[j] >> bshift), sh = (b & 1u) << 4;
             rk[j] = key[j] != sent ? (atomicAdd(&wc[w][b >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
         }
-        __syncthreads();
+        lds_sync();
         {
             // thread tid: buckets 2 tid, 2 tid + 1 (word tid of every wave's row)
             uint32_t run = 0;
@@ -616,7 +616,7 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
             }
             const uint32_t t0c = run & 0xFFFFu, t1c = run >> 16;
             uint32_t all;
-            const uint32_t ex = block_excl_scan<kBWaves>(t0c + t1c, wsum, &all);
+            const uint32_t ex = block_excl_scan<kBWaves, true>(t0c + t1c, wsum, &all);
             const uint32_t b0 = 2u * (uint32_t)tid, b1 = b0 + 1u;
             lbase[b0] = ex;
             lbase[b1] = ex + t0c;
@@ -628,7 +628,7 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
             gdst[b1] = b1 < nbe ? gbase[(uint64_t)ts.g * kNB + b1] + bf1 - (ex + t0c) : 0u;
             if (tid == 0) nvalid = all;
         }
-        __syncthreads();
+        lds_sync();
 #pragma unroll
         for (int j = 0; j < kEB; ++j) {
             if (key[j] != sent) {
@@ -636,13 +636,13 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
                 stage[lbase[b] + ((wc[w][b >> 1] >> sh) & 0xFFFFu) + rk[j]] = key[j];
             }
         }
-        __syncthreads();
+        lds_sync();
         const uint32_t nv = nvalid;
         for (uint32_t i = tid; i < nv; i += kBBlock) {
             const KeyT x = stage[i];
             out[gdst[(uint32_t)(x >> bshift)] + i] = x;
         }
-        __syncthreads();   // stage, gdst, tix are reused by the next tile
+        lds_sync();   // stage, gdst, tix are reused by the next tile
     }
 }
 
@@ -844,13 +844,13 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             const uint32_t R = (uint32_t)bshift + ceil_log2(ch.nb);
             auto pass = [&](int sh8, bool reload) __attribute__((always_inline)) {
                 for (int i = tid; i < kCWaves * 128; i += kCBlock) (&wc[0][0])[i] = 0;
-                __syncthreads();
+                lds_sync();
 #pragma unroll
                 for (int it = 0; it < PER; ++it) {
                     const uint32_t d = (uint32_t)(y[it] >> sh8) & 0xFFu, sh = (d & 1u) << 4;
                     rk[it] = (atomicAdd(&wc[w][d >> 1], 1u << sh) >> sh) & 0xFFFFu;
                 }
-                __syncthreads();
+                lds_sync();
                 if (w == 0) {
                     // lane: digits 4 lane .. 4 lane + 3 (words 2 lane, 2 lane + 1 of every wave's
                     // row).  Every counter becomes its keys' first slot: the digit's start
@@ -880,13 +880,13 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                         q1 += b[x];
                     }
                 }
-                __syncthreads();
+                lds_sync();
 #pragma unroll
                 for (int it = 0; it < PER; ++it) {
                     const uint32_t d = (uint32_t)(y[it] >> sh8) & 0xFFu, sh = (d & 1u) << 4;
                     stage[((wc[w][d >> 1] >> sh) & 0xFFFFu) + rk[it]] = y[it];
                 }
-                __syncthreads();
+                lds_sync();
                 if (reload) {
 #pragma unroll
                     for (int it = 0; it < PER; ++it) y[it] = srow[it * 64];
@@ -900,7 +900,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 if (np == 0) {   // one key value: already sorted
 #pragma unroll
                     for (int it = 0; it < PER; ++it) srow[it * 64] = y[it];
-                    __syncthreads();
+                    lds_sync();
                 }
                 for (int p = 0; p < np; ++p) {
                     pass(lo + 8 * p, p + 1 < np);
@@ -926,7 +926,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                     }
                 }
                 if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u);   // the sort's self-check
-                __syncthreads();
+                lds_sync();
                 if (!msd) break;
                 // runs of two or more keys start where a start bit is followed by a clear
                 // one: rare; the thread owning the start's word sorts the run and
@@ -971,7 +971,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 if (!again) break;
 #pragma unroll
                 for (int it = 0; it < PER; ++it) y[it] = srow[it * 64];
-                __syncthreads();
+                lds_sync();
             }
         }
         // ---------------------------------------------------- next chunk: its keys into y now
@@ -979,21 +979,27 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             const uint32_t x = atomicAdd(ticket, 1u);
             cid = order && x < total ? order[x] : x;
         }
-        __syncthreads();   // (nothing of this chunk is in flight yet)
+        lds_sync();   // (LDS-only: the last chunk's stores may still be in flight)
         const uint32_t cn = cid;
         Chunk chn;
         chn.ovf = kNoOvf;
         if (cn < total) {
             chn = chunks[cn];
             if (chn.ovf == kNoOvf) {
+                // every load unconditional (slots past the chunk re-read its last key), so
+                // the 32 loads leave back to back: a load under a lane test is a branch,
+                // and the compiler waits for each such load before the next one
                 uint32_t l = li0;
                 asm volatile("" : "+v"(l));   // per chunk: nothing derived from it is hoisted out of the loop
                 const int rem = (int)chn.nkeys - (int)l;
-                const KeyT* src = kb + chn.start + l;
+                const KeyT* src = kb + chn.start;
                 const KeyT bn = (KeyT)chn.blo << bshift;
+                const uint32_t lastk = chn.nkeys - 1u;   // nkeys >= 1
+#pragma unroll
+                for (int it = 0; it < PER; ++it) y[it] = src[min(l + (uint32_t)it * 64u, lastk)];
 #pragma unroll
                 for (int it = 0; it < PER; ++it)   // padding sorts last (all ones below R bits and above)
-                    y[it] = it * 64 < rem ? (KeyT)(src[it * 64] - bn) : (KeyT)~(KeyT)0;
+                    y[it] = it * 64 < rem ? (KeyT)(y[it] - bn) : (KeyT)~(KeyT)0;
             }
         }
         if (have && ch.ovf == kNoOvf) {
