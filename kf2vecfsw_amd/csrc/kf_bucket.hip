@@ -90,6 +90,21 @@ constexpr uint32_t kBkSlots = KF_BK_LAG ? 2u : 1u;   // record / meta / roff slo
 #ifndef KF_BK_PRIO
 #define KF_BK_PRIO 0
 #endif
+// Phase-1 staging slots (tools/ A/B builds): 1 = record position p goes to u16
+// slot p with bits 0 and 2 swapped inside its 8-record unit, so the consecutive
+// ranks one ds_add_rtn hands the lanes of a bucket land in different dwords
+// (banks) instead of pairs sharing one; phase 2 counts a unit in any order.
+// Measured and left off (profiles/r05/k11ab_*): phase-1 bank-conflict cycles
+// unchanged (1.050e9 -> 1.066e9 at k = 11: same-dword pairs are not conflicts),
+// VALU instructions +46 %, k = 11 8.59 -> 8.85 ms, k = 9/10/12 slower as well.
+#ifndef KF_BK_SWZ
+#define KF_BK_SWZ 0
+#endif
+__device__ __forceinline__ uint32_t stage_slot(uint32_t p) {
+    if (!KF_BK_SWZ) return p;
+    const uint32_t x = (p ^ (p >> 2)) & 1u;
+    return p ^ (x | (x << 2));
+}
 __device__ __forceinline__ void bk_setprio(uint32_t p) {   // p wave-uniform
     if (p == 0) __builtin_amdgcn_s_setprio(0);
     else if (p == 1) __builtin_amdgcn_s_setprio(1);
@@ -144,8 +159,11 @@ struct BkGeom {
 // CU): 8 shared counters 28.7 -> 7.3 with 64 replicas; 32: 13.7 -> 7.3; 128:
 // 11.2 -> 8.7 with 4.  In the kernel (profiles/r03/v5_lib_ab_k*_rank_replicas.json,
 // one process): k = 9 R = 32 6.39 ms (shared counters 9.05), k = 10 R = 16 7.27
-// (7.51); k = 11 stays at R = 1 (R = 4: 9.59 vs 9.24, its 512-entry tables cost
-// more than the conflicts they remove).  log2 R per k (KF_BK_RL<k>, tools/ only):
+// (7.51); k = 11 stays at R = 1: R = 4 measured 9.59 vs 9.24 in round 3 (its
+// 512-entry tables cost more than the conflicts they remove), and R = 2 leaves
+// phase 1's bank-conflict cycles where they were (1.05e9 -> 1.10e9) and its time
+// too (processes alternated: 8.58 vs 8.58 ms; profiles/r05/k11ab3_*).  log2 R
+// per k (KF_BK_RL<k>, tools/ only):
 #ifndef KF_BK_RL9
 #define KF_BK_RL9 5
 #endif
@@ -616,7 +634,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
 #pragma unroll
                     for (uint32_t x = 0; x < 7; ++x)
                         if (x < npad)
-                            *(volatile lds_u16*)(uintptr_t)(st + 2 * (e + x)) =
+                            *(volatile lds_u16*)(uintptr_t)(st + 2 * stage_slot(e + x)) =
                                 (uint16_t)((((bid(q) ^ 1u) & L::hmask) << L::bits) | ((e + x) & 63u));
                 }
             }
@@ -633,11 +651,11 @@ bucket_kernel(CountArgs A, BucketArgs B) {
 #if KF_BK_ABL == 4   // profiling only: no staging writes (wrong counts)
                     asm volatile("" ::"v"(rk[j]), "v"(s[j]));
 #else
-                    *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[j]) = (uint16_t)s[j];
+                    *(volatile lds_u16*)(uintptr_t)(st + 2 * stage_slot(rk[j])) = (uint16_t)s[j];
 #endif
                 }
                 if (s[15] != 0xFFFFFFFFu)
-                    *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[15]) = (uint16_t)s[15];
+                    *(volatile lds_u16*)(uintptr_t)(st + 2 * stage_slot(rk[15])) = (uint16_t)s[15];
             } else if (have) {
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
@@ -645,7 +663,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
                     if (s[j] != 0xFFFFFFFFu)
-                        *(volatile lds_u16*)(uintptr_t)(st + 2 * rk[j]) = (uint16_t)s[j];
+                        *(volatile lds_u16*)(uintptr_t)(st + 2 * stage_slot(rk[j])) = (uint16_t)s[j];
             }
             t_prev = T;
             off_prev = off;
@@ -1119,6 +1137,10 @@ int ensure_workspace(DevState& d, int dev, int k, int32_t n_genomes) {
         if (hipMalloc(&d.scratch, need) != hipSuccess)
             return kf_fail(KF_EHIP, "hipMalloc of %zu bytes of bucket scratch failed", need);
         d.scratch_bytes = need;
+#ifdef KF_PROFILE_BUILD
+        if (getenv("KF_BUCKET_DEBUG"))   // profiling builds: where the scratch landed
+            fprintf(stderr, "[kf_bucket] scratch %p (%zu B)\n", d.scratch, need);
+#endif
     }
     if (d.pstart_n < (size_t)n_genomes + 1) {
         const size_t cap = std::max((size_t)n_genomes + 1, 2 * d.pstart_n);

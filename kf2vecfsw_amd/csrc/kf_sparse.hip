@@ -784,7 +784,8 @@ __device__ __forceinline__ uint32_t ceil_log2(uint32_t x) { return x <= 1 ? 0u :
 // learns the genome's distinct k-mers before it by look-back, and every head
 // writes (key, distance to the next head), consecutive lanes at consecutive
 // outputs.  The next chunk's keys are loaded into the (dead) key registers as
-// soon as a chunk is sorted, so their latency hides behind the encoding.
+// soon as a chunk is sorted and first used when its sort starts, so their
+// latency hides behind the encoding.
 template <typename KeyT>
 __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restrict__ kb, const KeyT* __restrict__ ovf,
                                                             const Chunk* chunks, const uint32_t* cfirst, int n,
@@ -823,24 +824,44 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
     KeyT* srow = stage + li0;
     KeyT y[PER];
     uint32_t rk[PER];
-    uint32_t c = 0xFFFFFFFFu;   // the chunk being worked on (none before the first ticket)
+    // Tickets run one chunk ahead: while chunk c is sorted, the next chunk cn's
+    // descriptor and genome are already loading, its keys are loaded right after
+    // the sort, and the ticket of the chunk after it is taken then and published
+    // (cid) at the chunk's last barrier, so no step waits on a global round trip.
+    auto take = [&](uint32_t x) -> uint32_t { return order && x < total ? order[x] : x; };
+    if (tid == 0) cid = take(atomicAdd(ticket, 1u));
+    __syncthreads();
+    uint32_t cn = cid;          // the next chunk (>= total: none)
+    uint32_t c = 0xFFFFFFFFu;   // the chunk being worked on (none in the first iteration)
     Chunk ch;
     ch.ovf = kNoOvf;
+    uint32_t g = 0, c0 = 0;
+    bool last = false;
     for (;;) {
         const bool have = c < total;
-        uint32_t g = 0, c0 = 0, nk = 0;
-        bool last = false;
+        // (vector loads: an LDS-only barrier waits for scalar loads, not for these)
+        Chunk chn;
+        chn.ovf = kNoOvf;
+        uint32_t gn = 0;
+        if (cn < total) {   // used after this chunk's sort
+            chn = chunks[cn];
+            gn = cfirst[n + 2 + cn];
+        }
+        uint32_t nk = 0;
         KeyT base = 0;
         if (have) {
             tick(-1);
-            g = cfirst[n + 2 + c];
-            c0 = cfirst[g];
-            last = c + 1 == cfirst[g + 1];
             nk = ch.nkeys;
             base = (KeyT)ch.blo << bshift;
         }
         if (have && ch.ovf == kNoOvf) {
             // ------------------------------------------------ in-LDS sort (y loaded)
+            {
+                const int rem = (int)nk - (int)li0;
+#pragma unroll
+                for (int it = 0; it < PER; ++it)   // padding sorts last (all ones below R bits and above)
+                    y[it] = it * 64 < rem ? (KeyT)(y[it] - base) : (KeyT)~(KeyT)0;
+            }
             const uint32_t R = (uint32_t)bshift + ceil_log2(ch.nb);
             auto pass = [&](int sh8, bool reload) __attribute__((always_inline)) {
                 for (int i = tid; i < kCWaves * 128; i += kCBlock) (&wc[0][0])[i] = 0;
@@ -975,31 +996,23 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
             }
         }
         // ---------------------------------------------------- next chunk: its keys into y now
-        if (tid == 0) {
-            const uint32_t x = atomicAdd(ticket, 1u);
-            cid = order && x < total ? order[x] : x;
-        }
-        lds_sync();   // (LDS-only: the last chunk's stores may still be in flight)
-        const uint32_t cn = cid;
-        Chunk chn;
-        chn.ovf = kNoOvf;
+        uint32_t xt = 0, c0n = 0, c1n = 0;
         if (cn < total) {
-            chn = chunks[cn];
+            if (tid == 0) xt = atomicAdd(ticket, 1u);   // the chunk after cn (published at the end)
+            c0n = cfirst[gn];
+            c1n = cfirst[gn + 1];
             if (chn.ovf == kNoOvf) {
                 // every load unconditional (slots past the chunk re-read its last key), so
                 // the 32 loads leave back to back: a load under a lane test is a branch,
                 // and the compiler waits for each such load before the next one
+                // (raw keys: the base is taken off when the sort starts, so nothing
+                // waits for these loads before then)
                 uint32_t l = li0;
                 asm volatile("" : "+v"(l));   // per chunk: nothing derived from it is hoisted out of the loop
-                const int rem = (int)chn.nkeys - (int)l;
                 const KeyT* src = kb + chn.start;
-                const KeyT bn = (KeyT)chn.blo << bshift;
                 const uint32_t lastk = chn.nkeys - 1u;   // nkeys >= 1
 #pragma unroll
                 for (int it = 0; it < PER; ++it) y[it] = src[min(l + (uint32_t)it * 64u, lastk)];
-#pragma unroll
-                for (int it = 0; it < PER; ++it)   // padding sorts last (all ones below R bits and above)
-                    y[it] = it * 64 < rem ? (KeyT)(y[it] - bn) : (KeyT)~(KeyT)0;
             }
         }
         if (have && ch.ovf == kNoOvf) {
@@ -1034,6 +1047,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 okeys[o0 + j] = (uint64_t)(srow[it * 64] + base);
                 ocounts[o0 + j] = min(nx, nk) - i;
             }
+            if (tid == 0 && cn < total) cid = take(xt);
             lds_sync();   // stage, masks, cid are reused by the next chunk
             tick(5);
         } else if (have) {
@@ -1086,6 +1100,13 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
             }
+            if (tid == 0 && cn < total) cid = take(xt);
+            __syncthreads();
+        } else {
+            // no chunk yet (first iteration): every thread has read cid by now
+            lds_sync();
+            if (tid == 0 && cn < total) cid = take(xt);
+            lds_sync();
         }
         if (cn >= total) {
             if (prof && tid == 0)
@@ -1094,6 +1115,10 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
         }
         c = cn;
         ch = chn;
+        g = gn;
+        c0 = c0n;
+        last = cn + 1 == c1n;
+        cn = cid;
     }
 }
 
