@@ -1113,8 +1113,6 @@ int bucket_launch_info(int k, int* grid, int* block, int* lds) {
 int ensure_workspace(DevState& d, int dev, int k, int32_t n_genomes) {
     void* fn = bucket_kernel_for(k);
     if (!fn) return kf_fail(KF_EINVAL, "no bucket kernel for k=%d", k);
-    int rc = ensure_tables(d, k);
-    if (rc) return rc;
     const uint32_t lds = bucket_lds_for(k);
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
@@ -1129,6 +1127,12 @@ int ensure_workspace(DevState& d, int dev, int k, int32_t n_genomes) {
     size_t rec_b = 0, meta_b = 0, roff_b = 0;
     scratch_layout(d.cus, rec_b, meta_b, roff_b);
     const size_t need = rec_b + meta_b + roff_b;
+#ifdef KF_PROFILE_BUILD
+    if (getenv("KF_BUCKET_TABLES_FIRST")) {
+        const int rc = ensure_tables(d, k);
+        if (rc) return rc;
+    }
+#endif
     if (d.scratch_bytes < need) {
         if (d.scratch && (hipDeviceSynchronize() != hipSuccess || hipFree(d.scratch) != hipSuccess))
             return kf_fail(KF_EHIP, "hipFree of bucket scratch failed");
@@ -1137,11 +1141,23 @@ int ensure_workspace(DevState& d, int dev, int k, int32_t n_genomes) {
         if (hipMalloc(&d.scratch, need) != hipSuccess)
             return kf_fail(KF_EHIP, "hipMalloc of %zu bytes of bucket scratch failed", need);
         d.scratch_bytes = need;
-#ifdef KF_PROFILE_BUILD
-        if (getenv("KF_BUCKET_DEBUG"))   // profiling builds: where the scratch landed
-            fprintf(stderr, "[kf_bucket] scratch %p (%zu B)\n", d.scratch, need);
-#endif
     }
+    // the tables after the scratch (KF_BUCKET_TABLES_FIRST=1, profiling builds:
+    // before it, the order of rounds 2-4)
+#ifdef KF_PROFILE_BUILD
+    const bool tables_first = getenv("KF_BUCKET_TABLES_FIRST") != nullptr;
+#else
+    const bool tables_first = false;
+#endif
+    if (!tables_first) {
+        const int rc = ensure_tables(d, k);
+        if (rc) return rc;
+    }
+#ifdef KF_PROFILE_BUILD
+    if (getenv("KF_BUCKET_DEBUG"))   // profiling builds: where the scratch and tables landed
+        fprintf(stderr, "[kf_bucket] scratch %p (%zu B) col_idx %p bcol %p\n", d.scratch, d.scratch_bytes,
+                (void*)d.col_idx[k], (void*)d.bcol[k]);
+#endif
     if (d.pstart_n < (size_t)n_genomes + 1) {
         const size_t cap = std::max((size_t)n_genomes + 1, 2 * d.pstart_n);
         if (d.pstart && (hipDeviceSynchronize() != hipSuccess || hipFree(d.pstart) != hipSuccess))

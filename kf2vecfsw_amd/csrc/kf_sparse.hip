@@ -71,12 +71,19 @@ constexpr int kBWaves = kBBlock / 64;          // 8
 constexpr int kBD = 10;
 constexpr uint32_t kNB = 1u << kBD;
 __host__ __device__ constexpr int sp_dbits(int k) { return 2 * k < kBD ? 2 * k : kBD; }
-// Phase C: chunks of at most C keys (128 KiB of LDS), 1024 threads.
-constexpr int kCBlock = 512;   // 8 waves: 32 keys per thread, up to 256 VGPRs (1024 threads spilled at 128)
+// Phase C: chunks of at most 32 keys per thread (16,384 at 512 threads: 128 KiB
+// of LDS for u64 keys), up to 256 VGPRs per thread (1024 threads spilled at 128).
+// KF_SP_CBLOCK = 256 (tools/ A/B builds): 8,192-key chunks, two workgroups per CU.
+#ifndef KF_SP_CBLOCK
+#define KF_SP_CBLOCK 512
+#endif
+constexpr int kCBlock = KF_SP_CBLOCK;
 constexpr int kCWaves = kCBlock / 64;
+constexpr uint32_t kCCap = 32u * (uint32_t)kCBlock;
+constexpr int kCPerCU = 512 / kCBlock;   // resident chunk workgroups per CU
 template <typename KeyT>
 struct ChunkOf {
-    static constexpr uint32_t cap = 16384;                          // keys (128 KiB of u64, 64 KiB of u32)
+    static constexpr uint32_t cap = kCCap;                          // keys
     static constexpr int per = cap / kCBlock;                       // keys per thread
     static constexpr uint32_t wave_span = cap / kCWaves;
 };
@@ -373,15 +380,20 @@ __device__ __forceinline__ uint32_t lookback(uint64_t* status, uint32_t stride, 
 }
 
 // ---- LSD passes (the overflow sort of big buckets; round 4's sort of whole genomes)
-// gall[(p * n + g) * 256 + d] += keys of segment g with digit d in pass p.
+// gall[(p * n + g) * 256 + d] += keys of segment g with digit d in pass p: bits
+// [p bits, min((p + 1) bits, sbits)) of the key, the same digit the scatter of
+// pass p takes (a big bucket's keys carry its bucket index above sbits, so the
+// last pass's digit must stop at sbits too).
 // Workgroups loop over the segments (most are empty when nothing overflows).
 template <typename KeyT>
 __global__ void __launch_bounds__(kSBlock) sp_ghist_kernel(const KeyT* __restrict__ keys, const uint64_t* goff,
                                                            const uint32_t* tfirst, int n, int passes, int bits,
-                                                           uint32_t* gall) {
+                                                           int sbits, uint32_t* gall) {
     __shared__ uint32_t cnt[8][256];
     if (tfirst[n + 1] & 1u) return;   // invalid goff (sp_tiles_kernel): nothing is counted
     const uint32_t dmask = (1u << bits) - 1u;
+    const int lshift = (passes - 1) * bits;
+    const uint32_t lmask = (1u << (sbits - lshift)) - 1u;   // the last pass's digit
     for (int g = blockIdx.x; g < n; g += gridDim.x) {
         const uint32_t c0 = (uint32_t)goff[g], c1 = (uint32_t)goff[g + 1];
         if (c0 >= c1) continue;   // uniform
@@ -395,7 +407,8 @@ __global__ void __launch_bounds__(kSBlock) sp_ghist_kernel(const KeyT* __restric
 #pragma unroll
             for (int j = 0; j < kB; ++j) {
                 if (base + j * kSBlock + threadIdx.x < c1) {
-                    for (int p = 0; p < passes; ++p) atomicAdd(&cnt[p][(uint32_t)(x[j] >> (p * bits)) & dmask], 1u);
+                    for (int p = 0; p < passes; ++p)
+                        atomicAdd(&cnt[p][(uint32_t)(x[j] >> (p * bits)) & (p + 1 < passes ? dmask : lmask)], 1u);
                 }
             }
         }
@@ -787,7 +800,7 @@ __device__ __forceinline__ uint32_t ceil_log2(uint32_t x) { return x <= 1 ? 0u :
 // soon as a chunk is sorted and first used when its sort starts, so their
 // latency hides behind the encoding.
 template <typename KeyT>
-__global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restrict__ kb, const KeyT* __restrict__ ovf,
+__global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2))) sp2_chunk_kernel(const KeyT* __restrict__ kb, const KeyT* __restrict__ ovf,
                                                             const Chunk* chunks, const uint32_t* cfirst, int n,
                                                             int bshift, const uint64_t* goff, uint32_t* flags,
                                                             uint64_t* cstatus, uint32_t* ticket,
@@ -946,7 +959,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                         hh[(i >> 5) + 1] = (uint32_t)(bh >> 32);
                     }
                 }
-                if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u);   // the sort's self-check
+                if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u | 16u);   // the sort's self-check
                 lds_sync();
                 if (!msd) break;
                 // runs of two or more keys start where a start bit is followed by a clear
@@ -1060,7 +1073,7 @@ __global__ void __launch_bounds__(kCBlock) sp2_chunk_kernel(const KeyT* __restri
                 cnt += (i == 0 || a != pv) ? 1u : 0u;
                 disorder |= a < pv;
             }
-            if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u);
+            if (__ballot(disorder) && lane == 0) atomicOr(flags, 2u | 32u);
             uint32_t nu;
             (void)block_excl_scan<kCWaves>(cnt, wsum, &nu);
             if (tid == 0) {
@@ -1149,7 +1162,7 @@ uint64_t al256(uint64_t x) { return (x + 255) & ~255ull; }
 SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
     SpLayout L;
     const uint64_t ks = k <= 16 ? 4 : 8;
-    const uint64_t cap = 16384;   // ChunkOf<KeyT>::cap
+    const uint64_t cap = kCCap;   // ChunkOf<KeyT>::cap
     L.tiles = (uint32_t)(batch_bytes / kTB + (uint64_t)n + 1);
     // greedy packing: two consecutive chunks hold more than cap keys together
     L.cmax = (uint32_t)(2 * batch_bytes / cap + (uint64_t)n + 1);
@@ -1290,7 +1303,7 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
                            (const uint64_t*)nullptr, 0u, TileOf<KeyT>::tile, at32(L.oxlo));
         uint32_t* gall = at32(L.ogall);
         hipLaunchKernelGGL(sp_ghist_kernel<KeyT>, dim3((uint32_t)min(S, 4 * cus)), dim3(kSBlock), 0, s, src, seg_off,
-                           otfirst, S, passes, bits, gall);
+                           otfirst, S, passes, bits, B, gall);
         uint32_t* oorder = nullptr;
         if (S > 1 && S <= KF_SPARSE_ORDER_MAXN) {
             oorder = at32(L.oorder);
@@ -1324,7 +1337,7 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     if (pe && *pe == '1' && (hipMalloc((void**)&prof, 64) != hipSuccess || hipMemsetAsync(prof, 0, 64, s) != hipSuccess))
         return kf_fail(KF_EHIP, "profile buffer");
 #endif
-    hipLaunchKernelGGL(sp2_chunk_kernel<KeyT>, dim3((uint32_t)cus), dim3(kCBlock), ChunkOf<KeyT>::cap * sizeof(KeyT), s,
+    hipLaunchKernelGGL(sp2_chunk_kernel<KeyT>, dim3((uint32_t)(cus * kCPerCU)), dim3(kCBlock), ChunkOf<KeyT>::cap * sizeof(KeyT), s,
                        kb, ovf, (const Chunk*)(work + L.chunks), at32(L.cfirst), n, B, d_goff, &tfirst[n + 1],
                        (uint64_t*)(work + L.cstatus), at32(L.cticket), corder, d_keys, d_counts,
                        (uint64_t*)(work + L.unq), prof);
@@ -1339,6 +1352,14 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
         fprintf(stderr, "[kf_sparse k=%d] chunk kernel, cycles summed over workgroups (thread 0): pass0+load %.3g "
                 "pass1 %.3g fixup %.3g heads %.3g lookback %.3g stores %.3g\n", k, (double)h[0], (double)h[1],
                 (double)h[2], (double)h[3], (double)h[4], (double)h[5]);
+    }
+    if (getenv("KF_SPARSE_DEBUG")) {   // which check flagged the call (2: any; 16: chunk order; 32: big-bucket order)
+        uint32_t f[2] = {0, 0};
+        if (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&f[0], &tfirst[n + 1], 4, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(&f[1], oflags, 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return kf_fail(KF_EHIP, "debug readback");
+        fprintf(stderr, "[kf_sparse k=%d] flags main 0x%x overflow 0x%x (passes %d, big keys area %u segments)\n", k,
+                f[0], f[1], passes, L.smax);
     }
 #endif
     hipLaunchKernelGGL(sp2_final_kernel, dim3((n + 255) / 256), dim3(256), 0, s, tfirst, n, oflags,

@@ -160,3 +160,33 @@ def test_sparse_bench_size_every_genome(torch_dev, oracle, k):
         assert np.array_equal(gk[a: a + m], ek[a: a + m]), (k, g)
         assert np.array_equal(gc[a: a + m], ec[a: a + m]), (k, g)
         assert int(ec[a: a + m].sum(dtype=np.uint64)) == L - k + 1
+
+
+@pytest.mark.parametrize("k", [16, 31])
+def test_sparse_many_big_buckets_every_genome(torch_dev, oracle, k):
+    """Genomes long enough that their low buckets (canonical keys skew low: the
+    minimum of a code and its reverse complement) exceed a chunk: 6 x 24 Mbp, so
+    hundreds of big buckets go through the overflow sort beside ordinary chunks
+    in one call. Every genome bit-exact against the oracle (get_kmers,
+    kf2vec/main.py:133-172)."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    n, L = 6, 24_000_000
+    db = C.synth_device_batch(n, L, SEED + 7, width=80, device=torch_dev)
+    off = C.synth_layout(n, L)
+    sc = C.SparseCounter(k, torch_dev)
+    keys, cnts, nu = sc.count(db, int(off[-1]))
+    torch.cuda.synchronize()
+    gk = keys.cpu().numpy().view(np.uint64)
+    gc = cnts.cpu().numpy().view(np.uint32)
+    gn = nu.cpu().numpy().view(np.uint64)
+    host = db.data.cpu().numpy()
+    del keys, cnts, nu, db, sc
+    torch.cuda.empty_cache()
+    ek, ec, en = oracle.sparse_count_many(host[: int(off[-1])], off, k, 1, host_threads())
+    assert np.array_equal(gn, en), (gn[:4], en[:4])
+    for g in range(n):
+        a, m = int(off[g]), int(en[g])
+        assert np.array_equal(gk[a: a + m], ek[a: a + m]), (k, g)
+        assert np.array_equal(gc[a: a + m], ec[a: a + m]), (k, g)
+        assert int(ec[a: a + m].sum(dtype=np.uint64)) == L - k + 1
