@@ -221,8 +221,13 @@ struct BucketArgs {
     uint16_t* meta;            // gridDim.x * (nbk+1) * rmax round bucket offsets
     uint32_t* roff;            // gridDim.x * rmax round record offsets
     uint32_t accumulate;
+    uint32_t skew;              // record slot i starts skew x hash(i) (0..63) records later
     unsigned long long* prof;   // optional (KF_BUCKET_PROFILE): per-workgroup phase cycles
 };
+// Record slot i of the scratch (one per workgroup and lag slot).
+__device__ __forceinline__ uint16_t* rec_slot(const BucketArgs& B, uint64_t i, uint64_t cap) {
+    return B.rec + i * cap + (uint64_t)(((uint32_t)i * 0x9E3779B1u) >> 26) * B.skew;
+}
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -436,7 +441,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
     for (uint32_t it = 0; it < nmine + lag; ++it) {
       if (it < nmine) {
         const uint32_t slot = kLagK ? (it & 1u) : 0u;
-        uint16_t* rec = B.rec + ((uint64_t)blockIdx.x * kBkSlots + slot) * L::rec_cap;
+        uint16_t* rec = rec_slot(B, (uint64_t)blockIdx.x * kBkSlots + slot, L::rec_cap);
         uint16_t* meta = B.meta + ((uint64_t)blockIdx.x * kBkSlots + slot) * (NBK + 1) * L::rmax;
         uint32_t* roff = B.roff + ((uint64_t)blockIdx.x * kBkSlots + slot) * L::rmax;
         const Piece P = piece_at(blockIdx.x + it * gridDim.x);
@@ -686,7 +691,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
       }
       if (it >= lag) {
         const uint32_t slot = kLagK ? ((it - lag) & 1u) : 0u;
-        uint16_t* rec = B.rec + ((uint64_t)blockIdx.x * kBkSlots + slot) * L::rec_cap;
+        uint16_t* rec = rec_slot(B, (uint64_t)blockIdx.x * kBkSlots + slot, L::rec_cap);
         uint16_t* meta = B.meta + ((uint64_t)blockIdx.x * kBkSlots + slot) * (NBK + 1) * L::rmax;
         uint32_t* roff = B.roff + ((uint64_t)blockIdx.x * kBkSlots + slot) * L::rmax;
         const Piece P = piece_at(blockIdx.x + (it - lag) * gridDim.x);
@@ -1076,13 +1081,22 @@ int ensure_tables(DevState& d, int k) {
 
 // Scratch of one device: records, round metadata, round offsets, sized for the
 // largest of the compiled geometries (so a launch at another k reuses it).
+// Record slot skew in records (profiling builds: KF_BUCKET_SKEW, bytes).
+uint32_t rec_skew() {
+#ifdef KF_PROFILE_BUILD
+    const char* e = getenv("KF_BUCKET_SKEW");
+    return e ? (uint32_t)(strtoul(e, nullptr, 0) / 2) : 0u;
+#else
+    return 0u;
+#endif
+}
 void scratch_layout(int cus, size_t& rec_b, size_t& meta_b, size_t& roff_b) {
     rec_b = meta_b = roff_b = 0;
     for (int kk = 9; kk <= KF_MAX_K; ++kk) {   // the bucket kernels: k >= 9
         const size_t g = (size_t)cus * (16 / bucket_waves_for(kk)) * kBkSlots;
         bucket_geom(kk, [&](auto b) {
             using Lk = decltype(b);
-            rec_b = std::max(rec_b, g * (size_t)Lk::rec_cap * 2);
+            rec_b = std::max(rec_b, g * (size_t)Lk::rec_cap * 2 + (size_t)128 * rec_skew());
             meta_b = std::max(meta_b, g * ((size_t)Lk::nbk + 1) * Lk::rmax * 2);
             roff_b = std::max(roff_b, g * (size_t)Lk::rmax * 4);
             return 0;
@@ -1138,6 +1152,10 @@ int ensure_workspace(DevState& d, int dev, int k, int32_t n_genomes) {
             return kf_fail(KF_EHIP, "hipFree of bucket scratch failed");
         d.scratch = nullptr;
         d.scratch_bytes = 0;
+#ifdef KF_PROFILE_BUILD
+        // profiling builds: KF_BUCKET_CONTIG=1 asks for physically contiguous scratch
+        if (!(getenv("KF_BUCKET_CONTIG") && hipExtMallocWithFlags(&d.scratch, need, hipDeviceMallocContiguous) == hipSuccess))
+#endif
         if (hipMalloc(&d.scratch, need) != hipSuccess)
             return kf_fail(KF_EHIP, "hipMalloc of %zu bytes of bucket scratch failed", need);
         d.scratch_bytes = need;
@@ -1204,6 +1222,7 @@ int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s) {
     B.meta = (uint16_t*)((char*)d.scratch + rec_b);
     B.roff = (uint32_t*)((char*)d.scratch + rec_b + meta_b);
     B.accumulate = (flags & KF_ACCUMULATE) ? 1u : 0u;
+    B.skew = rec_skew();
     B.prof = nullptr;
 #ifdef KF_PROFILE_BUILD
     const char* pe = getenv("KF_BUCKET_PROFILE");   // debugging aid: synchronous, prints to stderr

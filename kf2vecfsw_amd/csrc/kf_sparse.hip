@@ -88,6 +88,11 @@ struct ChunkOf {
     static constexpr uint32_t wave_span = cap / kCWaves;
 };
 constexpr uint32_t kNoOvf = 0xFFFFFFFFu;
+// 8-bit MSD passes over the top bits of a chunk's keys before the run fix-up
+// (tools/ A/B builds: KF_SP_MSD=3 sorts 24 bits, leaving almost no runs).
+#ifndef KF_SP_MSD
+#define KF_SP_MSD 2
+#endif
 struct Chunk {          // one LDS sort unit: buckets [blo, blo + nb) of one genome
     uint32_t start;     // first slot in the bucketed keys
     uint32_t nkeys;
@@ -141,16 +146,24 @@ __device__ __forceinline__ bool tile_span(const uint64_t* goff, const uint32_t* 
 // every outstanding global access of the wave first).
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Inclusive prefix sum over a whole (fully active) wave on the VALU: DPP row
+// shifts and row broadcasts instead of __shfl_up's six ds_bpermute round trips.
+__device__ __forceinline__ uint32_t wave_incl_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+
 // Exclusive prefix of one value per thread over an NW-wave workgroup; *total
 // (optional) gets the sum.  Contains two barriers (LDS-only ones if LDSB).
 template <int NW, bool LDSB = false>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total = nullptr) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = v;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
-        if (lane >= d) inc += o;
-    }
+    const uint32_t inc = wave_incl_dpp(v);
     if (lane == 63) wsum[w] = inc;
     if (LDSB) lds_sync();
     else __syncthreads();
@@ -899,12 +912,7 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
                     }
                     const uint32_t d0 = r0 & 0xFFFFu, d1 = r0 >> 16, d2 = r1 & 0xFFFFu;
                     const uint32_t sum = d0 + d1 + d2 + (r1 >> 16);
-                    uint32_t inc = sum;
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
-                        if (lane >= d) inc += o;
-                    }
-                    const uint32_t ex = inc - sum;
+                    const uint32_t ex = wave_incl_dpp(sum) - sum;
                     uint32_t q0 = ex | ((ex + d0) << 16), q1 = (ex + d0 + d1) | ((ex + d0 + d1 + d2) << 16);
 #pragma unroll
                     for (int x = 0; x < kCWaves; ++x) {
@@ -928,9 +936,9 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
             };
             constexpr uint32_t kRun = 32;
             for (int round = 0; round < 2; ++round) {
-                const bool msd = round == 0 && R > 16;
-                const int lo = msd ? (int)R - 16 : 0;
-                const int np = msd ? 2 : (int)((R + 7) / 8);
+                const bool msd = round == 0 && R > 8 * KF_SP_MSD;
+                const int lo = msd ? (int)R - 8 * KF_SP_MSD : 0;
+                const int np = msd ? KF_SP_MSD : (int)((R + 7) / 8);
                 if (np == 0) {   // one key value: already sorted
 #pragma unroll
                     for (int it = 0; it < PER; ++it) srow[it * 64] = y[it];
