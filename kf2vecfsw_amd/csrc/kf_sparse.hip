@@ -93,6 +93,18 @@ constexpr uint32_t kNoOvf = 0xFFFFFFFFu;
 #ifndef KF_SP_MSD
 #define KF_SP_MSD 2
 #endif
+// Digit width of the chunk sort's passes (KF_SP_DIGIT = 8 or 10): 10-bit MSD
+// passes sort the top 20 bits, so a 16,384-key chunk over 2^20 values leaves
+// runs of equal top bits for ~1.6 % of its keys instead of ~22 %, and k <= 15
+// chunks are sorted whole in two passes.  64 x 5 Mbp (profiles/r05/v19_*):
+// k = 31 7.69 -> 7.23 ms, k = 13 6.37 -> 5.97 (fix-up 0.69e9 -> 0.38e9 cycles,
+// the passes unchanged; 16 KiB of counters per workgroup instead of 4).
+#ifndef KF_SP_DIGIT
+#define KF_SP_DIGIT 10
+#endif
+constexpr int kDB = KF_SP_DIGIT;
+constexpr uint32_t kND = 1u << kDB;          // digits
+constexpr uint32_t kNWW = kND / 2;           // packed u16 counter words per wave
 struct Chunk {          // one LDS sort unit: buckets [blo, blo + nb) of one genome
     uint32_t start;     // first slot in the bucketed keys
     uint32_t nkeys;
@@ -795,13 +807,14 @@ __device__ __forceinline__ uint32_t ceil_log2(uint32_t x) { return x <= 1 ? 0u :
 // ---- C2. chunk sort + run-length encoding (persistent, one 512-thread
 // workgroup per CU).  A chunk's keys (minus its first bucket's base: R = B +
 // ceil(log2 nb) bits) are loaded striped, 32 per thread, and sorted in LDS by
-// stable 8-bit passes: per pass a returning packed-u16 LDS add per key into its
-// wave's digit counter (stable: an LDS unit serves one instruction's lanes in
-// lane order, and keys are striped so lane, then iteration, then wave is slot
-// order), one wave turns the 256 x 8 counters into slots, the keys go to their
-// slots and come back striped.  For R > 16 only the top 16 bits are sorted that
-// way (two passes): a chunk of <= 16,384 keys over 65,536 values of those bits
-// leaves runs of a few keys with equal top bits, each sorted by the thread
+// stable 10-bit passes (KF_SP_DIGIT): per pass a returning packed-u16 LDS add per
+// key into its wave's digit counter (stable: an LDS unit serves one
+// instruction's lanes in lane order, and keys are striped so lane, then
+// iteration, then wave is slot order), every thread turns two digits' 8 counters
+// into slots (a block scan over the digits), the keys go to their slots and come
+// back striped.  For R > 20 only the top 20 bits are sorted that way (two
+// passes): a chunk of <= 16,384 keys over 2^20 values of those bits leaves a few
+// runs of keys with equal top bits, each sorted by the thread
 // owning the mask word of its start (insertion sort in LDS); a run longer than
 // kRun whose keys are not all equal (repeats make long runs of EQUAL keys, which
 // need nothing) sends the chunk through every pass (LSD takes any order).  One
@@ -823,8 +836,9 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
     using CO = ChunkOf<KeyT>;
     constexpr int PER = CO::per;
     constexpr uint32_t kWords = CO::cap / 32;   // mask words of a chunk
-    static_assert(kWords == (uint32_t)kCBlock && kCWaves * 128 >= 2 * kWords, "one mask word per thread");
-    __shared__ uint32_t wc[kCWaves][128];   // packed u16 digit counters per wave; after the sort: start | head masks
+    static_assert(kWords == (uint32_t)kCBlock && kCWaves * kNWW >= 2 * kWords && kNWW <= (uint32_t)kCBlock,
+                  "one mask word per thread");
+    __shared__ uint32_t wc[kCWaves][kNWW];   // packed u16 digit counters per wave; after the sort: start | head masks
     __shared__ uint32_t wpre[kWords];       // heads before each head-mask word
     __shared__ uint32_t wsum[kCWaves];
     __shared__ uint32_t cid, before_s;
@@ -890,42 +904,41 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
             }
             const uint32_t R = (uint32_t)bshift + ceil_log2(ch.nb);
             auto pass = [&](int sh8, bool reload) __attribute__((always_inline)) {
-                for (int i = tid; i < kCWaves * 128; i += kCBlock) (&wc[0][0])[i] = 0;
+                for (int i = tid; i < kCWaves * (int)kNWW; i += kCBlock) (&wc[0][0])[i] = 0;
                 lds_sync();
 #pragma unroll
                 for (int it = 0; it < PER; ++it) {
-                    const uint32_t d = (uint32_t)(y[it] >> sh8) & 0xFFu, sh = (d & 1u) << 4;
+                    const uint32_t d = (uint32_t)(y[it] >> sh8) & (kND - 1u), sh = (d & 1u) << 4;
                     rk[it] = (atomicAdd(&wc[w][d >> 1], 1u << sh) >> sh) & 0xFFFFu;
                 }
                 lds_sync();
-                if (w == 0) {
-                    // lane: digits 4 lane .. 4 lane + 3 (words 2 lane, 2 lane + 1 of every wave's
-                    // row).  Every counter becomes its keys' first slot: the digit's start
+                {
+                    // thread t: digits 2t, 2t + 1 (word t of every wave's row), all waves at
+                    // once.  Every counter becomes its keys' first slot: the digit's start
                     // plus the counts of the earlier waves (packed halves: <= cap < 2^16).
-                    uint32_t a[kCWaves], b[kCWaves], r0 = 0, r1 = 0;
+                    const bool own = tid < (int)kNWW;
+                    const int j = own ? tid : 0;
+                    uint32_t a[kCWaves], r = 0;
 #pragma unroll
                     for (int x = 0; x < kCWaves; ++x) {
-                        a[x] = wc[x][2 * lane];
-                        b[x] = wc[x][2 * lane + 1];
-                        r0 += a[x];
-                        r1 += b[x];
+                        a[x] = own ? wc[x][j] : 0u;
+                        r += a[x];
                     }
-                    const uint32_t d0 = r0 & 0xFFFFu, d1 = r0 >> 16, d2 = r1 & 0xFFFFu;
-                    const uint32_t sum = d0 + d1 + d2 + (r1 >> 16);
-                    const uint32_t ex = wave_incl_dpp(sum) - sum;
-                    uint32_t q0 = ex | ((ex + d0) << 16), q1 = (ex + d0 + d1) | ((ex + d0 + d1 + d2) << 16);
+                    const uint32_t d0 = r & 0xFFFFu;
+                    const uint32_t ex = block_excl_scan<kCWaves, true>(d0 + (r >> 16), wsum);
+                    uint32_t q = ex | ((ex + d0) << 16);
+                    if (own) {
 #pragma unroll
-                    for (int x = 0; x < kCWaves; ++x) {
-                        wc[x][2 * lane] = q0;
-                        wc[x][2 * lane + 1] = q1;
-                        q0 += a[x];
-                        q1 += b[x];
+                        for (int x = 0; x < kCWaves; ++x) {
+                            wc[x][j] = q;
+                            q += a[x];
+                        }
                     }
                 }
                 lds_sync();
 #pragma unroll
                 for (int it = 0; it < PER; ++it) {
-                    const uint32_t d = (uint32_t)(y[it] >> sh8) & 0xFFu, sh = (d & 1u) << 4;
+                    const uint32_t d = (uint32_t)(y[it] >> sh8) & (kND - 1u), sh = (d & 1u) << 4;
                     stage[((wc[w][d >> 1] >> sh) & 0xFFFFu) + rk[it]] = y[it];
                 }
                 lds_sync();
@@ -936,16 +949,16 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
             };
             constexpr uint32_t kRun = 32;
             for (int round = 0; round < 2; ++round) {
-                const bool msd = round == 0 && R > 8 * KF_SP_MSD;
-                const int lo = msd ? (int)R - 8 * KF_SP_MSD : 0;
-                const int np = msd ? KF_SP_MSD : (int)((R + 7) / 8);
+                const bool msd = round == 0 && R > (uint32_t)(kDB * KF_SP_MSD);
+                const int lo = msd ? (int)R - kDB * KF_SP_MSD : 0;
+                const int np = msd ? KF_SP_MSD : (int)((R + kDB - 1) / kDB);
                 if (np == 0) {   // one key value: already sorted
 #pragma unroll
                     for (int it = 0; it < PER; ++it) srow[it * 64] = y[it];
                     lds_sync();
                 }
                 for (int p = 0; p < np; ++p) {
-                    pass(lo + 8 * p, p + 1 < np);
+                    pass(lo + kDB * p, p + 1 < np);
                     tick(p == 0 ? 0 : 1);
                 }
                 // one striped sweep: run starts (the top bits above `lo` differ) and heads

@@ -64,14 +64,15 @@ def format_kf(name: str, counts: np.ndarray, pseudocount: bool = False, raw_cnt:
 
 
 def _pipeline_budget(paths: list[str], batch_gb) -> int:
-    """Bytes per batch: -batch_gb if given, else about an eighth of the input
-    (so reading, copying, counting and writing overlap; measured best of 4-16
-    parts on 64 x 5 Mbp, tools/e2e_bench.py) within [16 MiB, 4 GiB].
-    KF_BATCH_PARTS overrides the part count."""
+    """Bytes per batch: -batch_gb if given, else about a quarter of the input
+    (so reading, copying, counting and writing overlap; 64 x 5 Mbp on two boxes,
+    tools/e2e_bench.py: 4 parts 26.1 and 32.9 Gbases/s against 8 parts 22.5 and
+    29.8, profiles/r05/v19_e2e_parts.json, v6_e2e_variants.json) within
+    [16 MiB, 4 GiB].  KF_BATCH_PARTS overrides the part count."""
     if batch_gb:
         return int(float(batch_gb) * (1 << 30))
     total = sum(os.path.getsize(p) for p in paths)
-    parts = int(os.environ.get("KF_BATCH_PARTS", "8"))
+    parts = int(os.environ.get("KF_BATCH_PARTS", "4"))
     return int(min(max(total // parts, 16 << 20), 4 << 30))
 
 
