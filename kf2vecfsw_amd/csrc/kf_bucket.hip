@@ -39,7 +39,8 @@ namespace kf {
 // stay 0, so no records are written or read at all), 4 = no
 // phase-1 staging writes (dense path), 5 = no phase-2 histogram adds, 7 = rank
 // adds without returns, 8 = no phase 2 (rows stay zero), 9 = as 1 with
-// lane-consecutive flush slots (no LDS bank conflicts in the flush).
+// lane-consecutive flush slots (no LDS bank conflicts in the flush), 10 = no
+// barrier after each bucket's flush, 11 = no phase-2 barriers.
 #ifndef KF_BK_ABL
 #define KF_BK_ABL 0
 #endif
@@ -958,14 +959,18 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             }
             re_next = m;
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[0] += t - t0; t0 = t; }
+#if KF_BK_ABL != 11   // profiling only (11: no phase-2 barriers at all; wrong counts)
             lds_barrier();
+#endif
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[1] += t - t0; t0 = t; }
 #pragma unroll
             for (int x = 0; x < kFG; ++x) flush_cols((c0 & ~3u) + 4 * ((uint32_t)tid + x * L::block), ci[x], c0, c1);
             for (uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + kFG * L::block); g4 < c1; g4 += 4 * L::block)
                 flush_cols(g4, col_at(g4), c0, c1);
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[2] += t - t0; t0 = t; }
-            lds_barrier();
+#if KF_BK_ABL != 10 && KF_BK_ABL != 11   // profiling only (10: no barrier after the flush, the
+            lds_barrier();                     // bound of overlapping a flush with the next count)
+#endif
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[3] += t - t0; }
         }
         if (B.prof && lane == 0) {   // per wave: records, barrier, (phase-1 barrier), consume
