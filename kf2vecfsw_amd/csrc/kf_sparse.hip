@@ -99,6 +99,11 @@ constexpr uint32_t kNoOvf = 0xFFFFFFFFu;
 // chunks are sorted whole in two passes.  64 x 5 Mbp (profiles/r05/v19_*):
 // k = 31 7.69 -> 7.23 ms, k = 13 6.37 -> 5.97 (fix-up 0.69e9 -> 0.38e9 cycles,
 // the passes unchanged; 16 KiB of counters per workgroup instead of 4).
+// Phase A loads a workgroup's next tile's bytes while it makes this tile's keys
+// (KF_SP_PREFETCH_A=0: when the tile starts).
+#ifndef KF_SP_PREFETCH_A
+#define KF_SP_PREFETCH_A 1
+#endif
 #ifndef KF_SP_DIGIT
 #define KF_SP_DIGIT 10
 #endif
@@ -259,10 +264,32 @@ __global__ void __launch_bounds__(256) sp_tilemap_kernel(const uint64_t* goff, u
 // amortise the walk (up to k-1 + newline bytes).  out[] holds SENT on entry
 // (4^k - 1 = T..T, never canonical: its reverse complement A..A is smaller) and
 // keeps it where no window ends.
+// The bytes a thread's emit reads, loaded ahead: its kEB bytes and the kEB before
+// them, four 16-byte loads at addresses clamped into the buffer (every load
+// unconditional: the caller keeps them in flight while it finishes a tile).
+struct EmitIn {
+    uint4 a, b, c, d;
+};
+__device__ __forceinline__ EmitIn emit_load(const uint8_t* __restrict__ bytes, const TileSpan& ts, uint64_t nbytes) {
+    EmitIn e;
+    if (nbytes < 2 * kEB) {   // (uniform) a tiny batch: emit_row reads byte by byte
+        e.a = e.b = e.c = e.d = make_uint4(0u, 0u, 0u, 0u);
+        return e;
+    }
+    const uint64_t lim = (nbytes - 2 * kEB) & ~15ull;
+    const uint64_t p0 = (uint64_t)ts.base + threadIdx.x * kEB;
+    const uint64_t pm = min(p0, lim), pc = min(p0 >= kEB ? p0 - kEB : 0ull, lim);
+    e.a = *(const uint4*)(bytes + pm);
+    e.b = *(const uint4*)(bytes + pm + 16);
+    e.c = *(const uint4*)(bytes + pc);
+    e.d = *(const uint4*)(bytes + pc + 16);
+    return e;
+}
+
 template <typename KeyT>
 __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, const TileSpan& ts, uint32_t tix,
                                          uint32_t n_excl, const uint64_t* excl, const uint32_t* xlo, int k,
-                                         KeyT (&out)[kEB]) {
+                                         uint64_t nbytes, const EmitIn& in, KeyT (&out)[kEB]) {
     const uint32_t q0 = threadIdx.x * kEB;
     if (q0 >= ts.cnt) return;
     const uint32_t p0 = ts.base + q0, cnt = min((uint32_t)kEB, ts.cnt - q0);
@@ -271,8 +298,9 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
     const int hi = 2 * k - 2;
     uint32_t code[kEB];
     bool any = false;
-    if (cnt == (uint32_t)kEB && ((uintptr_t)(bytes + p0) & 15u) == 0) {   // two 16-byte loads
-        const uint4 a = *(const uint4*)(bytes + p0), b = *(const uint4*)(bytes + p0 + 16);
+    // (emit_load's clamp never moves a full, 16-byte aligned row: p0 + 2 kEB <= nbytes)
+    if (cnt == (uint32_t)kEB && (p0 & 15u) == 0 && (uint64_t)p0 + 2 * kEB <= nbytes) {   // the preloaded row
+        const uint4 a = in.a, b = in.b;
         const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
         for (int j = 0; j < kEB; ++j) {
@@ -305,10 +333,11 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
     int m = 0;
     uint64_t q = p0;
     bool open = true;   // the walk may go on
-    if (p0 >= floor_ + kEB && (p0 & 15u) == 0) {
-        // the kEB bytes before p0 in two 16-byte loads (no chain of dependent
-        // byte loads), walked in registers
-        const uint4 a = *(const uint4*)(bytes + p0 - kEB), b = *(const uint4*)(bytes + p0 - 16);
+    if (p0 >= floor_ + kEB && (p0 & 15u) == 0 && (uint64_t)p0 - kEB <= ((nbytes - 2 * kEB) & ~15ull) &&
+        nbytes >= 2 * kEB) {
+        // the kEB bytes before p0, preloaded (no chain of dependent byte loads),
+        // walked in registers
+        const uint4 a = in.c, b = in.d;
         const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
         for (int j = kEB - 1; j >= 0; --j) {
@@ -327,9 +356,20 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
         back |= (W)c << (2 * m);
         ++m;
     }
-    W fw = back, rc = 0;   // fw: the m context bases, most recent lowest
+    W fw = back, rc;   // fw: the m context bases, most recent lowest
     int len = m;
-    for (int i = 0; i < m; ++i) rc |= (W)(3u - ((uint32_t)(back >> (2 * i)) & 3u)) << (hi - 2 * i);
+    {
+        // rc: the context's reverse complement, most recent base's complement at
+        // bits hi..hi+1: complement the m pairs, reverse the pair order of the word
+        // (bit reversal, then swap the two bits of every pair), align to k pairs
+        const W cm = m ? (W)(back ^ ((W)~(W)0 >> (8 * sizeof(W) - 2 * m))) : (W)0;
+        W r;
+        if constexpr (sizeof(W) == 8) r = (W)__builtin_bitreverse64((uint64_t)cm);
+        else r = (W)__builtin_bitreverse32((uint32_t)cm);
+        const W m55 = (W)0x5555555555555555ull;
+        r = ((r >> 1) & m55) | ((r & m55) << 1);
+        rc = r >> (8 * sizeof(W) - 2 * k);
+    }
     // the next excluded range's bounds (the thread's bytes rarely meet one)
     uint64_t xs = ix < n_excl ? excl[2 * ix] : ~0ull, xe = ix < n_excl ? excl[2 * ix + 1] : ~0ull;
     // one step of the window, without branches: a base rolls in, '\n' (4) is
@@ -561,7 +601,7 @@ template <typename KeyT>
 __global__ void __launch_bounds__(kBBlock) sp2_count_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
                                                             const uint32_t* tfirst, int n, const uint64_t* excl,
                                                             uint32_t n_excl, const uint32_t* xlo, int k, int bshift,
-                                                            uint32_t* gtot) {
+                                                            uint64_t nbytes, uint32_t* gtot) {
     __shared__ uint32_t h[kNB];
     if (tfirst[n + 1] & 1u) return;   // invalid goff: nothing is counted
     const int g = blockIdx.x;
@@ -570,16 +610,32 @@ __global__ void __launch_bounds__(kBBlock) sp2_count_kernel(const uint8_t* __res
     for (uint32_t i = threadIdx.x; i < kNB; i += kBBlock) h[i] = 0;
     __syncthreads();
     const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
+    TileSpan ts;
+    tile_span(goff, tfirst, n, t0 + blockIdx.y, ts, kTB);
+    EmitIn in = emit_load(bytes, ts, nbytes);
     for (uint32_t t = t0 + blockIdx.y; t < t1; t += gridDim.y) {
-        TileSpan ts;
-        tile_span(goff, tfirst, n, t, ts, kTB);
+        // this workgroup's next tile's bytes go out before this tile's keys are made
+        // (KF_SP_PREFETCH_A=0, tools/ builds: loaded when the tile starts)
+        TileSpan tn = ts;
+        EmitIn inn = in;
+        if (!KF_SP_PREFETCH_A) in = emit_load(bytes, ts, nbytes);
+        if (KF_SP_PREFETCH_A && t + gridDim.y < t1) {
+            tile_span(goff, tfirst, n, t + gridDim.y, tn, kTB);
+            inn = emit_load(bytes, tn, nbytes);
+        }
         KeyT out[kEB];
 #pragma unroll
         for (int j = 0; j < kEB; ++j) out[j] = sent;
-        emit_row(bytes, ts, t, n_excl, excl, xlo, k, out);
+        emit_row(bytes, ts, t, n_excl, excl, xlo, k, nbytes, in, out);
 #pragma unroll
         for (int j = 0; j < kEB; ++j)
             if (out[j] != sent) atomicAdd(&h[(uint32_t)(out[j] >> bshift)], 1u);
+        if (KF_SP_PREFETCH_A) {
+            ts = tn;
+            in = inn;
+        } else if (t + gridDim.y < t1) {
+            tile_span(goff, tfirst, n, t + gridDim.y, ts, kTB);
+        }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < kNB; i += kBBlock)
@@ -608,9 +664,9 @@ template <typename KeyT>
 __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __restrict__ bytes, const uint64_t* goff,
                                                               uint32_t* tfirst, int n, const uint64_t* excl,
                                                               uint32_t n_excl, const uint32_t* xlo, int k,
-                                                              int bshift, const uint32_t* gbase, uint64_t* status,
+                                                              int bshift, uint64_t nbytes, const uint32_t* gbase, uint64_t* status,
                                                               uint32_t* ticket, const uint32_t* order,
-                                                              KeyT* __restrict__ out) {
+                                                              KeyT* __restrict__ out, unsigned long long* prof) {
     __shared__ uint32_t wc[kBWaves][kNB / 2];   // per wave: packed u16 bucket counts, then the wave's base
     __shared__ uint32_t lbase[kNB];             // tile-local start of each bucket
     __shared__ uint32_t gdst[kNB];              // slot of the bucket's first key in this tile, minus lbase
@@ -621,21 +677,51 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
     const int tid = threadIdx.x, w = tid >> 6;
     const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
     const uint32_t nbe = 1u << sp_dbits(k);
-    for (;;) {
-        if (tid == 0) {
-            const uint32_t x = atomicAdd(ticket, 1u);
-            tix = order && x < tfirst[n] ? order[x] : x;
+    // KF_SPARSE_PROFILE (profiling builds): thread 0's cycles per phase, summed
+    // over workgroups: ticket + emit, rank, scan + look-back, stage, stores
+    unsigned long long pt[5] = {0, 0, 0, 0, 0}, tmark = 0;
+    auto tick = [&](int ph) {
+        if (prof && tid == 0) {
+            const unsigned long long tn = __builtin_amdgcn_s_memtime();
+            if (ph >= 0) pt[ph] += tn - tmark;
+            tmark = tn;
         }
-        lds_sync();
-        const uint32_t t = tix;
-        TileSpan ts;
-        if (!tile_span(goff, tfirst, n, t, ts, kTB)) return;   // uniform: no tiles left
+    };
+    // Tickets run one tile ahead (as the chunk kernel's): the next tile's bytes are
+    // loaded as soon as this tile's keys are made, and stay in flight through its
+    // ranks, look-back, re-order and stores; the ticket after that is taken then
+    // and published (tix) at the tile's last barrier.
+    auto take = [&](uint32_t x) -> uint32_t { return order && x < tfirst[n] ? order[x] : x; };
+    if (tid == 0) tix = take(atomicAdd(ticket, 1u));
+    __syncthreads();
+    uint32_t t = tix;
+    __syncthreads();   // every thread has t before tix changes
+    TileSpan ts{0u, 0u, 0u, 0u, 0u};
+    bool have = tile_span(goff, tfirst, n, t, ts, kTB);
+    EmitIn in = emit_load(bytes, ts, nbytes);
+    if (tid == 0 && have) tix = take(atomicAdd(ticket, 1u));
+    __syncthreads();
+    uint32_t tn = tix;
+    for (;;) {
+        tick(-1);
+        if (!have) {   // uniform: no tiles left
+            if (prof && tid == 0)
+                for (int x = 0; x < 5; ++x) atomicAdd(&prof[x], pt[x]);
+            return;
+        }
         KeyT key[kEB];
 #pragma unroll
         for (int j = 0; j < kEB; ++j) key[j] = sent;
-        emit_row(bytes, ts, t, n_excl, excl, xlo, k, key);
+        emit_row(bytes, ts, t, n_excl, excl, xlo, k, nbytes, in, key);
+        TileSpan tsn{0u, 0u, 0u, 0u, 0u};
+        const bool hn = tile_span(goff, tfirst, n, tn, tsn, kTB);
+        EmitIn inn = in;
+        if (hn) inn = emit_load(bytes, tsn, nbytes);
+        uint32_t xt = 0;
+        if (tid == 0 && hn) xt = atomicAdd(ticket, 1u);   // the tile after tn (published at the end)
         for (int i = tid; i < kBWaves * (int)kNB / 2; i += kBBlock) (&wc[0][0])[i] = 0;
         lds_sync();
+        tick(0);
         uint32_t rk[kEB];
 #pragma unroll
         for (int j = 0; j < kEB; ++j) {
@@ -643,6 +729,7 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
             rk[j] = key[j] != sent ? (atomicAdd(&wc[w][b >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
         }
         lds_sync();
+        tick(1);
         {
             // thread tid: buckets 2 tid, 2 tid + 1 (word tid of every wave's row)
             uint32_t run = 0;
@@ -667,6 +754,7 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
             if (tid == 0) nvalid = all;
         }
         lds_sync();
+        tick(2);
 #pragma unroll
         for (int j = 0; j < kEB; ++j) {
             if (key[j] != sent) {
@@ -675,12 +763,20 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
             }
         }
         lds_sync();
+        tick(3);
         const uint32_t nv = nvalid;
         for (uint32_t i = tid; i < nv; i += kBBlock) {
             const KeyT x = stage[i];
             out[gdst[(uint32_t)(x >> bshift)] + i] = x;
         }
+        if (tid == 0 && hn) tix = take(xt);
         lds_sync();   // stage, gdst, tix are reused by the next tile
+        tick(4);
+        t = tn;
+        ts = tsn;
+        have = hn;
+        in = inn;
+        tn = tix;
     }
 }
 
@@ -1280,9 +1376,15 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     // A: genome x bucket totals
     const uint32_t slices = (uint32_t)max(1, min(64, 1024 / max(1, (int)n)));
     hipLaunchKernelGGL(sp2_count_kernel<KeyT>, dim3((uint32_t)n, slices), dim3(kBBlock), 0, s, d_bytes, d_goff, tfirst,
-                       n, d_excl, (uint32_t)n_excl, xlo, k, B, at32(L.gtot));
+                       n, d_excl, (uint32_t)n_excl, xlo, k, B, batch_bytes, at32(L.gtot));
     hipLaunchKernelGGL(sp2_gbase_kernel, dim3((uint32_t)n), dim3(1024), 0, s, d_goff, at32(L.gtot), n, at32(L.gbase),
                        at32(L.gkeys));
+    unsigned long long* prof = nullptr;   // [0, 8): chunk kernel phases, [8, 16): bucket scatter phases
+#ifdef KF_PROFILE_BUILD
+    const char* pe = getenv("KF_SPARSE_PROFILE");   // debugging aid: synchronous, prints to stderr
+    if (pe && *pe == '1' && (hipMalloc((void**)&prof, 128) != hipSuccess || hipMemsetAsync(prof, 0, 128, s) != hipSuccess))
+        return kf_fail(KF_EHIP, "profile buffer");
+#endif
     // B: scatter by bucket
     uint32_t* border = nullptr;
     if (n > 1 && n <= KF_SPARSE_ORDER_MAXN) {
@@ -1292,8 +1394,8 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     KeyT* kb = (KeyT*)(work + L.kb);
     KeyT* ovf = (KeyT*)(work + L.ovf);
     hipLaunchKernelGGL(sp2_scatter_kernel<KeyT>, dim3((uint32_t)cus), dim3(kBBlock), kTB * sizeof(KeyT), s, d_bytes,
-                       d_goff, tfirst, n, d_excl, (uint32_t)n_excl, xlo, k, B, at32(L.gbase),
-                       (uint64_t*)(work + L.bstatus), at32(L.bticket), border, kb);
+                       d_goff, tfirst, n, d_excl, (uint32_t)n_excl, xlo, k, B, batch_bytes, at32(L.gbase),
+                       (uint64_t*)(work + L.bstatus), at32(L.bticket), border, kb, prof ? prof + 8 : nullptr);
     // C0: chunk plan
     const uint32_t cap = ChunkOf<KeyT>::cap;
     uint64_t* seg_off = (uint64_t*)(work + L.seg_off);
@@ -1352,12 +1454,6 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
         corder = at32(L.corder);
         hipLaunchKernelGGL(sp_order_kernel, dim3(L.cmax / kSBlock + 1), dim3(kSBlock), 0, s, at32(L.cfirst), n, corder);
     }
-    unsigned long long* prof = nullptr;
-#ifdef KF_PROFILE_BUILD
-    const char* pe = getenv("KF_SPARSE_PROFILE");   // debugging aid: synchronous, prints to stderr
-    if (pe && *pe == '1' && (hipMalloc((void**)&prof, 64) != hipSuccess || hipMemsetAsync(prof, 0, 64, s) != hipSuccess))
-        return kf_fail(KF_EHIP, "profile buffer");
-#endif
     hipLaunchKernelGGL(sp2_chunk_kernel<KeyT>, dim3((uint32_t)(cus * kCPerCU)), dim3(kCBlock), ChunkOf<KeyT>::cap * sizeof(KeyT), s,
                        kb, ovf, (const Chunk*)(work + L.chunks), at32(L.cfirst), n, B, d_goff, &tfirst[n + 1],
                        (uint64_t*)(work + L.cstatus), at32(L.cticket), corder, d_keys, d_counts,
@@ -1366,13 +1462,16 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
     const uint32_t* oflags = passes > 0 ? at32(L.otfirst) + L.smax + 1 : &tfirst[n + 1];
 #ifdef KF_PROFILE_BUILD
     if (prof) {
-        unsigned long long h[8] = {0};
-        if (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(h, prof, 56, hipMemcpyDeviceToHost) != hipSuccess)
+        unsigned long long h[16] = {0};
+        if (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(h, prof, 128, hipMemcpyDeviceToHost) != hipSuccess)
             return kf_fail(KF_EHIP, "profile readback");
         (void)hipFree(prof);
         fprintf(stderr, "[kf_sparse k=%d] chunk kernel, cycles summed over workgroups (thread 0): pass0+load %.3g "
                 "pass1 %.3g fixup %.3g heads %.3g lookback %.3g stores %.3g\n", k, (double)h[0], (double)h[1],
                 (double)h[2], (double)h[3], (double)h[4], (double)h[5]);
+        fprintf(stderr, "[kf_sparse k=%d] bucket scatter, cycles summed over workgroups (thread 0): ticket+emit %.3g "
+                "rank %.3g scan+lookback %.3g stage %.3g stores %.3g\n", k, (double)h[8], (double)h[9],
+                (double)h[10], (double)h[11], (double)h[12]);
     }
     if (getenv("KF_SPARSE_DEBUG")) {   // which check flagged the call (2: any; 16: chunk order; 32: big-bucket order)
         uint32_t f[2] = {0, 0};
