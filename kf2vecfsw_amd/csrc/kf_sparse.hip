@@ -104,6 +104,13 @@ constexpr uint32_t kNoOvf = 0xFFFFFFFFu;
 #ifndef KF_SP_PREFETCH_A
 #define KF_SP_PREFETCH_A 1
 #endif
+// Unroll of the chunk kernel's mask sweep and run-length stores (tools/ A/B).
+#ifndef KF_SP_UNROLL_SWEEP
+#define KF_SP_UNROLL_SWEEP 4
+#endif
+#ifndef KF_SP_UNROLL_STORES
+#define KF_SP_UNROLL_STORES 4
+#endif
 #ifndef KF_SP_DIGIT
 #define KF_SP_DIGIT 10
 #endif
@@ -286,10 +293,14 @@ __device__ __forceinline__ EmitIn emit_load(const uint8_t* __restrict__ bytes, c
     return e;
 }
 
-template <typename KeyT>
+// BK (phase A): out[] gets each window's bucket (the key's top D = 2k - bshift
+// bits) instead of its key: the top bits of min(code, reverse complement) are the
+// min of the two top bits, so the reverse complement is kept as its top D bits
+// only (one 32-bit register) and out[] is 32-bit (fewer VGPRs for u64 keys).
+template <typename KeyT, bool BK = false, typename OutT = KeyT>
 __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, const TileSpan& ts, uint32_t tix,
                                          uint32_t n_excl, const uint64_t* excl, const uint32_t* xlo, int k,
-                                         uint64_t nbytes, const EmitIn& in, KeyT (&out)[kEB]) {
+                                         uint64_t nbytes, const EmitIn& in, OutT (&out)[kEB], int bshift = 0) {
     const uint32_t q0 = threadIdx.x * kEB;
     if (q0 >= ts.cnt) return;
     const uint32_t p0 = ts.base + q0, cnt = min((uint32_t)kEB, ts.cnt - q0);
@@ -370,6 +381,8 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
         r = ((r >> 1) & m55) | ((r & m55) << 1);
         rc = r >> (8 * sizeof(W) - 2 * k);
     }
+    const int dtop = 2 * k - bshift - 2;       // BK: the top pair's shift in the D-bit top
+    uint32_t rtop = (uint32_t)(rc >> bshift);  // BK: the reverse complement's top D bits
     // the next excluded range's bounds (the thread's bytes rarely meet one)
     uint64_t xs = ix < n_excl ? excl[2 * ix] : ~0ull, xe = ix < n_excl ? excl[2 * ix + 1] : ~0ull;
     // one step of the window, without branches: a base rolls in, '\n' (4) is
@@ -378,9 +391,15 @@ __device__ __forceinline__ void emit_row(const uint8_t* __restrict__ bytes, cons
         const bool isb = c < 4u;
         const uint32_t cb = c & 3u;
         fw = isb ? (W)(((fw << 2) | cb) & kmask) : fw;
-        rc = isb ? (W)((rc >> 2) | ((W)(3u - cb) << hi)) : rc;
         len = c == 5u ? 0 : len + (isb ? 1 : 0);
-        out[j] = isb && len >= k ? (KeyT)(fw < rc ? fw : rc) : out[j];
+        if constexpr (BK) {
+            rtop = isb ? (rtop >> 2) | ((3u - cb) << dtop) : rtop;
+            const uint32_t ft = (uint32_t)(fw >> bshift);
+            out[j] = isb && len >= k ? (OutT)min(ft, rtop) : out[j];
+        } else {
+            rc = isb ? (W)((rc >> 2) | ((W)(3u - cb) << hi)) : rc;
+            out[j] = isb && len >= k ? (OutT)(fw < rc ? fw : rc) : out[j];
+        }
     };
     if (xs >= (uint64_t)p0 + kEB) {   // no excluded byte here (bytes past cnt hold code 4)
 #pragma unroll
@@ -609,7 +628,6 @@ __global__ void __launch_bounds__(kBBlock) sp2_count_kernel(const uint8_t* __res
     if (t0 + blockIdx.y >= t1) return;   // uniform
     for (uint32_t i = threadIdx.x; i < kNB; i += kBBlock) h[i] = 0;
     __syncthreads();
-    const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
     TileSpan ts;
     tile_span(goff, tfirst, n, t0 + blockIdx.y, ts, kTB);
     EmitIn in = emit_load(bytes, ts, nbytes);
@@ -623,13 +641,24 @@ __global__ void __launch_bounds__(kBBlock) sp2_count_kernel(const uint8_t* __res
             tile_span(goff, tfirst, n, t + gridDim.y, tn, kTB);
             inn = emit_load(bytes, tn, nbytes);
         }
-        KeyT out[kEB];
+        if constexpr (sizeof(KeyT) == 8) {   // u64 keys: buckets only (146 VGPRs instead of 173)
+            uint32_t out[kEB];                  // (0xFFFFFFFF: no window ends here)
 #pragma unroll
-        for (int j = 0; j < kEB; ++j) out[j] = sent;
-        emit_row(bytes, ts, t, n_excl, excl, xlo, k, nbytes, in, out);
+            for (int j = 0; j < kEB; ++j) out[j] = 0xFFFFFFFFu;
+            emit_row<KeyT, true, uint32_t>(bytes, ts, t, n_excl, excl, xlo, k, nbytes, in, out, bshift);
 #pragma unroll
-        for (int j = 0; j < kEB; ++j)
-            if (out[j] != sent) atomicAdd(&h[(uint32_t)(out[j] >> bshift)], 1u);
+            for (int j = 0; j < kEB; ++j)
+                if (out[j] != 0xFFFFFFFFu) atomicAdd(&h[out[j]], 1u);
+        } else {                                // u32 keys: the keys themselves (fewer VGPRs so)
+            const KeyT sent = (KeyT)((1ull << (2 * k)) - 1);
+            KeyT out[kEB];
+#pragma unroll
+            for (int j = 0; j < kEB; ++j) out[j] = sent;
+            emit_row<KeyT>(bytes, ts, t, n_excl, excl, xlo, k, nbytes, in, out);
+#pragma unroll
+            for (int j = 0; j < kEB; ++j)
+                if (out[j] != sent) atomicAdd(&h[(uint32_t)(out[j] >> bshift)], 1u);
+        }
         if (KF_SP_PREFETCH_A) {
             ts = tn;
             in = inn;
@@ -712,7 +741,7 @@ __global__ void __launch_bounds__(kBBlock) sp2_scatter_kernel(const uint8_t* __r
         KeyT key[kEB];
 #pragma unroll
         for (int j = 0; j < kEB; ++j) key[j] = sent;
-        emit_row(bytes, ts, t, n_excl, excl, xlo, k, nbytes, in, key);
+        emit_row<KeyT>(bytes, ts, t, n_excl, excl, xlo, k, nbytes, in, key);
         TileSpan tsn{0u, 0u, 0u, 0u, 0u};
         const bool hn = tile_span(goff, tfirst, n, tn, tsn, kTB);
         EmitIn inn = in;
@@ -1061,7 +1090,7 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
                 // (the keys differ); the order check on the sorted bits (every key is in
                 // order when lo = 0).  Consecutive lanes read consecutive slots.
                 bool disorder = false;
-#pragma unroll 4
+#pragma unroll KF_SP_UNROLL_SWEEP
                 for (int it = 0; it < PER; ++it) {
                     const uint32_t i = li0 + (uint32_t)it * 64;
                     const KeyT v = srow[it * 64], pv = i ? stage[i - 1] : (KeyT)0;
@@ -1159,7 +1188,7 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
             lds_sync();
             tick(4);
             const uint64_t o0 = goff[g] + before_s;
-#pragma unroll 4
+#pragma unroll KF_SP_UNROLL_STORES
             for (int it = 0; it < PER; ++it) {
                 const uint32_t i = li0 + (uint32_t)it * 64;
                 if (i >= nk) continue;
