@@ -556,7 +556,9 @@ def sparse_bench(args, dev) -> dict:
     alg = nbytes + 12 * int(nuh.sum())
     key_b = 4 if k <= 16 else 8
     bucket_bits = min(10, 2 * k)
-    lds_passes = (2 * k - bucket_bits + 2 + 7) // 8   # a chunk spans ~2-4 buckets
+    r_bits = 2 * k - bucket_bits + 2                  # a chunk spans ~2-4 buckets
+    sort_note = ("two 10-bit passes (the whole key)" if r_bits <= 20 else
+                 "two 10-bit MSD passes over the top 20 bits + an in-LDS fix-up of runs of equal top bits")
     del keys, cnts, nu, db, sc, tot, c64
     torch.cuda.empty_cache()
     return {"config": f"get_kmers sparse counter, k={k}, {n} synthetic {L / 1e6:g} Mbp genomes resident in HBM "
@@ -568,8 +570,8 @@ def sparse_bench(args, dev) -> dict:
                          "alg_bytes_per_launch": alg,
                          "design_bytes_per_launch": int(nbytes * 2 + n * L * 2 * key_b + 12 * int(nuh.sum())),
                          "note": f"{2 * k}-bit keys: bucket count over the bytes, bucket scatter ({key_b} B per key "
-                                 f"out, top {bucket_bits} bits), per-chunk LDS sort ({lds_passes} passes of 8 bits "
-                                 f"in LDS, {key_b} B per key in) + run-length encoding (12 B per distinct k-mer out)"},
+                                 f"out, top {bucket_bits} bits), per-chunk LDS sort ({sort_note}, {key_b} B per key "
+                                 f"in) + run-length encoding (12 B per distinct k-mer out)"},
             "parity": "ok" if ok else "MISMATCH"}
 
 
