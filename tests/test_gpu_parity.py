@@ -476,11 +476,13 @@ def test_arbitrary_byte_values(torch_dev, oracle, k):
     check_against_oracle(oracle, blobs, k, counts, totals, fmt=1, tag="bytes")
 
 
-def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle):
+@pytest.mark.parametrize("k", [7, 9])
+def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, k):
     """k=7 K1x: its u16 LDS counters overflow on low-complexity sequence unless the
     drain path moves counts out exactly (poly-A, dinucleotide and satellite
     repeats, N-broken poly-A that fills the unpaired-window table, and FASTA lines
-    of 1-7 bases that keep every iteration on the irregular path)."""
+    of 1-7 bases that keep every iteration on the irregular path).  k=9: the
+    bucket kernel on the same inputs, where one bucket takes almost every record."""
     rng = np.random.default_rng(4242)
     sat = gen.random_seq(rng, 171).tobytes()
     polya = b"A" * 40_000_000
@@ -492,13 +494,13 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle):
         b">short\n" + gen.wrap(np.frombuffer(b"C" * 3_000_000, np.uint8), 7),
         b">t\n" + gen.wrap(gen.random_seq(rng, 500_000), 80),
     ]
-    counts, totals = run_batch(blobs, 7, torch_dev)
-    check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16")
+    counts, totals = run_batch(blobs, k, torch_dev)
+    check_against_oracle(oracle, blobs, k, counts, totals, tag="u16")
     # many genome pieces per workgroup, each above the drain threshold
     blobs = [b">p\n" + gen.wrap(np.frombuffer(b"T" * int(rng.integers(60_000, 400_000)), np.uint8), 70)
              for _ in range(300)]
-    counts, totals = run_batch(blobs, 7, torch_dev)
-    check_against_oracle(oracle, blobs, 7, counts, totals, tag="u16-many")
+    counts, totals = run_batch(blobs, k, torch_dev)
+    check_against_oracle(oracle, blobs, k, counts, totals, tag="u16-many")
 
 
 def test_k7_many_pieces_many_records(torch_dev, oracle):
