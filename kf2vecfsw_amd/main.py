@@ -736,7 +736,7 @@ def build_parser() -> argparse.ArgumentParser:
                     help="Computes k-mer counts with 0.5 pseudocount added to each frequency value")
     pf.add_argument("-raw_cnt", action="store_true", help="Computes raw k-mer counts without normalization")
     pf.add_argument("-batch_gb", type=float, default=None,
-                    help="Input bytes per device batch (GiB). Default: about 1/8 of the input, 16 MiB..4 GiB")
+                    help="Input bytes per device batch (GiB). Default: about a quarter of the input, 16 MiB..4 GiB")
     pf.add_argument("-device", default=None, help="torch device (default: cuda)")
     pf.add_argument("-gpus", type=int, default=1,
                     help="GPUs to shard the files over, one process each (0 = every visible GPU). Default: 1. "
