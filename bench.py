@@ -87,6 +87,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--secondary-k", type=int, default=11,
                     help="also time this k on the same batch (BASELINE configs[4]); 0 = off; N=1 only")
+    ap.add_argument("--by-k", default="3-12",
+                    help="also time every k of this range on the batch (N=1; '' = off): the reference's vocab "
+                         "branches k=3..10 (main.py:281-296) plus 11 and 12")
+    ap.add_argument("--by-k-steps", type=int, default=3)
     ap.add_argument("--verify", type=int, default=4, help="genomes per rank checked bit-exactly against the oracle")
     ap.add_argument("--e2e-genomes", type=int, default=64, help="CLI end-to-end files (0 = off; N=1 only)")
     ap.add_argument("--e2e-len", type=int, default=5_000_000)
@@ -117,24 +121,10 @@ def shard_plan(total: int, rank: int, world: int, per: int = SUB_BATCH) -> list[
 
 
 def usable_cpus() -> tuple[int, dict]:
-    """CPUs this process may run on: the affinity mask, capped by a cgroup v2/v1
-    CPU quota if one is set (a GPU box may show the whole host in the mask)."""
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    quota = None
-    try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if q != "max":
-            quota = float(q) / float(per)
-    except (OSError, ValueError):
-        try:
-            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
-            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
-            if q > 0:
-                quota = q / per
-        except (OSError, ValueError):
-            pass
-    n = aff if quota is None else max(1, min(aff, int(quota)))
-    return n, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_cpu_quota": quota}
+    """CPUs this process may use (kf2vecfsw_amd.main.usable_cpus: the affinity
+    mask capped by a cgroup CPU quota)."""
+    from kf2vecfsw_amd.main import usable_cpus as U
+    return U()
 
 
 def _oracle():
@@ -379,6 +369,50 @@ class Workload:
         return res
 
 
+def parse_k_range(spec: str) -> list[int]:
+    """"3-12" -> [3..12]; "7,9,11" -> [7, 9, 11]."""
+    ks = []
+    for part in str(spec).split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            ks += list(range(int(a), int(b) + 1))
+        else:
+            ks.append(int(part))
+    return ks
+
+
+def by_k_bench(W, dbs, args, workload_tag: str) -> dict:
+    """Every k of --by-k on the resident configs[1] batch:
+    1 warm-up + --by-k-steps timed kf_count_batch calls each, the kernel's HIP
+    event time per launch, its roofline (FASTA bytes + 4 B x bins per genome,
+    as the headline), the measured traffic when profiles/ holds it, and parity:
+    every total analytic plus 2 genomes bit-exact against the oracle."""
+    import torch
+    res = {}
+    for k in parse_k_range(args.by_k):
+        kc, o, el, ms, _ = W.run(k, args.by_k_steps, 1, dbs)
+        okk = W.verify(k, 0, o, 2)
+        km = float(np.mean(ms))
+        alg = (W.fasta_bytes + 4 * kc.nbins * W.n) / max(1, W.nsb)
+        tr, src = load_traffic(k, workload_tag)
+        grid, block, lds = kc.launch_info()
+        res[str(k)] = {"kernel_ms": round(km, 4), "kernel_ms_runs": [round(x, 4) for x in ms],
+                       "Gbases_s": round(W.n * args.seq_len / (km * 1e-3) / 1e9, 1),
+                       "nbins": kc.nbins, "alg_bytes_per_launch": int(alg),
+                       "roofline": {"bound": "hbm", "achieved": round(alg / (km * 1e-3) / 1e9, 1),
+                                    "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                                    "frac": round(alg / (km * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+                                    "traffic": tr, "traffic_source": src},
+                       "kernel": ("k1x_kernel<%d>" % k) if k <= 8 else ("bucket_kernel<%d>" % k),
+                       "launch": [grid, block, lds], "parity": "ok" if okk else "MISMATCH"}
+        del kc, o
+        torch.cuda.empty_cache()
+    return res
+
+
 def cold_launch_ms(torch, kc, db, stream, idle_s: float = 1.0) -> float:
     """One launch after the GPU has idled `idle_s` (what a CLI batch sees after host I/O)."""
     out = kc.alloc_out(db.n)
@@ -456,7 +490,9 @@ def e2e_bench(args, dev) -> dict:
             os.makedirs(out)
             with contextlib.redirect_stdout(io.StringIO()):
                 t0 = time.perf_counter()
-                M.main(["get_frequencies", "-input_dir", inp, "-output_dir", out, "-k", str(7), "-p", str(threads)])
+                # the default -p (mp.cpu_count(), as the reference): what a user gets; the
+                # CLI caps it at the usable CPUs (main.host_threads)
+                M.main(["get_frequencies", "-input_dir", inp, "-output_dir", out, "-k", str(7)])
                 return time.perf_counter() - t0
 
         # one warm run, then 7 timed: the host side (file reads on a shared box)
@@ -595,19 +631,22 @@ def resolve_world(args, env=None) -> tuple[int, bool]:
     return n, n > 1
 
 
-def spawn_ranks(n: int, argv: list[str], env=None) -> int:
+def spawn_ranks(n: int, argv: list[str], env=None, timeout_s: float | None = None) -> int:
     """`python bench.py --gpus N` without a launcher: start N rank processes
     (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1) -- exactly
     what torch.distributed.run would give them -- and relay rank 0's stdout.
     This process never touches the GPU (no HIP call before the children start;
     no exec).  If a rank fails, the others get 60 s to finish, then are
-    terminated by PID.  Returns the worst exit status (0 if all ranks passed)."""
+    terminated by PID; ranks still running after `timeout_s` (default
+    KF_BENCH_TIMEOUT_S or 1800 s) are terminated too, so a hung rank cannot
+    hold the run forever.  Returns the worst exit status (0 if all ranks
+    passed; 124 when the overall limit ended the run)."""
     import socket
     import subprocess
     import threading
     env = dict(os.environ if env is None else env)
     from kf2vecfsw_amd.main import visible_gpus   # KFD topology / *_VISIBLE_DEVICES, no HIP init
-    avail = visible_gpus()
+    avail = visible_gpus(env)   # the masks the children will see
     if env.get("KF_BENCH_REHEARSE") != "1" and avail is not None and n > avail:
         print(f"bench.py: --gpus {n} but only {avail} GPU(s) visible", file=sys.stderr)
         return 2
@@ -629,13 +668,18 @@ def spawn_ranks(n: int, argv: list[str], env=None) -> int:
     t = threading.Thread(target=relay, daemon=True)
     t.start()
     deadline = None
+    limit = float(timeout_s if timeout_s is not None else env.get("KF_BENCH_TIMEOUT_S", 1800))
+    hard = time.monotonic() + limit
+    timed_out = False
     while True:
         rcs = [p.poll() for p in procs]
         if all(rc is not None for rc in rcs):
             break
         if deadline is None and any(rc not in (None, 0) for rc in rcs):
             deadline = time.monotonic() + 60.0
-        if deadline is not None and time.monotonic() > deadline:
+        over = time.monotonic() > hard
+        if over or (deadline is not None and time.monotonic() > deadline):
+            timed_out = over
             for p in procs:
                 if p.poll() is None:
                     p.terminate()
@@ -649,6 +693,9 @@ def spawn_ranks(n: int, argv: list[str], env=None) -> int:
     t.join(timeout=10)
     rcs = [p.wait() for p in procs]
     bad = [(r, rc) for r, rc in enumerate(rcs) if rc]
+    if timed_out:
+        print(f"bench.py: ranks still running after {limit:g} s were terminated", file=sys.stderr)
+        return 124
     if bad:
         print("bench.py: rank(s) failed: " + ", ".join(f"rank {r} exit {rc}" for r, rc in bad), file=sys.stderr)
         return max(abs(rc) for _, rc in bad) or 1
@@ -736,7 +783,9 @@ def main() -> None:
                "seq_len": args.seq_len, "line_width": 80, "sub_batches_per_gpu": nsb,
                "sub_batch": args.sub_batch, "resident": resident,
                "parallelism": f"round-robin genome shards x{world}, no collective"}
-    cfg.update({"kernel_grid": [grid, block], "lds_bytes": lds})
+    # what ONE kf_count_batch launch of this rank holds (the largest sub-batch)
+    cfg.update({"kernel_grid": [grid, block], "lds_bytes": lds,
+                "genomes_per_launch": max(c for _, _, c in W.plan), "bytes_per_launch": max(W.sb_bytes)})
     wm = m["warm_ms"]
     out = {
         "metric": "Gbases/s k-mer→.kf build at k=7; achieved HBM GB/s vs gfx950 peak",
@@ -796,6 +845,10 @@ def main() -> None:
             "parity": "ok" if ok2 else "MISMATCH"}
         out["parity"] = "ok" if ok else "MISMATCH"
         del o2
+    if args.by_k and world == 1 and resident:
+        out["by_k"] = by_k_bench(W, dbs, args, workload_tag)
+        ok &= all(v["parity"] == "ok" for v in out["by_k"].values())
+        out["parity"] = "ok" if ok else "MISMATCH"
     del dbs, first, m
     if rank == 0 and world == 1 and args.e2e_genomes:
         torch.cuda.empty_cache()

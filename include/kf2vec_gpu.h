@@ -163,9 +163,15 @@ int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
  * kf_count_batch.  Genome g's results are d_keys[goff[g] + i] and
  * d_counts[goff[g] + i] for i < d_nuniq[g] (a genome has at most goff[g+1] -
  * goff[g] distinct k-mers, so both arrays hold batch_bytes = goff[n] entries).
- * The device sorts the windows' keys (segmented LSD radix sort of 2k bits) in
- * d_work, which must hold kf_sparse_workspace_bytes(k, batch_bytes, n_genomes)
- * bytes; d_keys is also used as sort scratch.  batch_bytes < 2^32 and d_bytes
+ * The device counts each genome's keys per bucket (their top min(10, 2k)
+ * bits), scatters every window's key once into its bucket (decoupled
+ * look-back per bucket), packs whole buckets into chunks of <= 16,384 keys and
+ * sorts each chunk in LDS (10-bit MSD passes plus a fix-up of runs of equal
+ * top bits); buckets larger than a chunk are sorted by LSD passes in an
+ * overflow area.  Then run-length encoding.  d_work must hold
+ * kf_sparse_workspace_bytes(k, batch_bytes, n_genomes) bytes: two key areas of
+ * 4 (k <= 16) or 8 B per input byte plus ~1 B per byte of tables, so with the
+ * outputs a call needs ~21 (k <= 16) or ~29 device bytes per input byte.  batch_bytes < 2^32 and d_bytes
  * 16-byte aligned (KF_EINVAL otherwise, as kf_count_batch).
  * Asynchronous on `stream`, no allocation, no host synchronisation.  The
  * offsets are checked on the device: if d_goff decreases or d_goff[n] >

@@ -72,12 +72,29 @@ def build(force: bool = False, verbose: bool = False, ablation: bool = False, ou
 
 HEADERS = ["kf_internal.h", "kf_front.h", "../../include/kf2vec_gpu.h"]
 
+_TOOLCHAIN: list[bytes] = []
+
+
+def _toolchain_id() -> bytes:
+    """The compilers' identity (`hipcc --version`, `g++ --version`, once per
+    process): part of every object's cache key, so a toolchain upgrade never
+    relinks stale objects."""
+    if not _TOOLCHAIN:
+        out = b""
+        for cmd in ([HIPCC, "--version"], ["g++", "--version"]):
+            try:
+                out += subprocess.run(cmd, capture_output=True, check=False).stdout
+            except OSError:
+                out += b"missing:" + cmd[0].encode()
+        _TOOLCHAIN.append(out)
+    return _TOOLCHAIN[0]
+
 
 def _object(src: str, cmd_tail: list[str]) -> tuple[str, bool]:
     """Object path for `src` compiled with `cmd_tail`, keyed by the hash of the
-    source, the shared headers and the command (so an edit rebuilds only the
-    objects it touches); and whether it already exists."""
-    h = hashlib.sha256(" ".join(cmd_tail).encode())
+    source, the shared headers, the command and the compilers' versions (so an
+    edit rebuilds only the objects it touches); and whether it already exists."""
+    h = hashlib.sha256(" ".join(cmd_tail).encode() + b"\0" + _toolchain_id())
     for d in [src] + HEADERS:
         with open(os.path.join(CSRC, d), "rb") as f:
             h.update(f.read())

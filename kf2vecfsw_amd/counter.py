@@ -73,13 +73,12 @@ def index_records(data: np.ndarray, fmt: int = N.KF_FMT_AUTO, base: int = 0) -> 
 @dataclasses.dataclass
 class HostBatch:
     """Genomes packed back to back: genome g = data[off[g]:off[g+1]]."""
-    data: torch.Tensor | None   # uint8, (pinned) host; None: registered files already on the device
+    data: torch.Tensor | None   # uint8, (pinned) host
     off: np.ndarray             # uint64 [n+1]
     excl: np.ndarray | None     # uint64 [2*m] absolute [start, end) pairs; None: FASTA indexed on the device
     names: list[str]
     dev_data: torch.Tensor | None = None   # the bytes already copied to the device (maybe on another stream)
     dev_event: object = None               # ... and the event that copy recorded
-    reg: object = None                     # RegisteredFiles to release once the copies ran
 
     @property
     def n(self) -> int:
@@ -187,76 +186,6 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
     return HostBatch(data, off, ex.astype(np.uint64), list(names) if names else list(paths))
 
 
-class RegisteredFiles:
-    """The files of a batch mapped (mmap) and page-locked in place
-    (hipHostRegister), so the DMA engine copies them from the page cache: no host
-    memcpy of the bytes.  release() after the copies ran."""
-
-    def __init__(self):
-        self.maps: list = []   # (mmap, numpy view, registered pointer or 0)
-
-    def add(self, path: str, size: int):
-        import mmap
-        fd = os.open(path, os.O_RDONLY)
-        try:
-            m = mmap.mmap(fd, size, prot=mmap.PROT_READ)
-        finally:
-            os.close(fd)
-        a = np.frombuffer(m, dtype=np.uint8)
-        rc = int(torch.cuda.cudart().cudaHostRegister(a.ctypes.data, size, 0))   # hipHostRegisterDefault
-        self.maps.append((m, a, a.ctypes.data if rc == 0 else 0))
-        if rc != 0:
-            raise N.NativeError(f"hipHostRegister failed ({rc}) on {path}")
-        return a
-
-    def release(self) -> None:
-        cr = torch.cuda.cudart()
-        for m, a, ptr in self.maps:
-            if ptr:
-                cr.cudaHostUnregister(ptr)
-        self.maps = []
-
-
-def pack_files_registered(paths: Sequence[str], names: Sequence[str], device: torch.device, stream,
-                          fmt: int = N.KF_FMT_AUTO) -> HostBatch:
-    """As pack_files, but the bytes go from each file's page-cache pages straight
-    to a device batch buffer on `stream` (mmap + hipHostRegister; '\n' padding
-    between genomes filled on the device).  FASTQ files are indexed on the host
-    from the mapping; a batch of FASTA files leaves its record index to the
-    device (excl None).  The returned batch carries `reg` (release it once the
-    copies have run: after dev_event)."""
-    sizes = [os.path.getsize(p) for p in paths]
-    off = _layout(sizes)
-    reg = RegisteredFiles()
-    excl, fastq = [], False
-    with torch.cuda.stream(stream):
-        dev = torch.empty(max(int(off[-1]), ALIGN) + ALIGN, dtype=torch.uint8, device=device)
-        dev.fill_(10)
-        for i, p in enumerate(paths):
-            if sizes[i] == 0:
-                excl.append(np.zeros(0, np.uint64))
-                continue
-            a = reg.add(p, sizes[i])
-            lo = int(off[i])
-            dev[lo: lo + sizes[i]].copy_(torch.from_numpy(a), non_blocking=True)
-            if fmt == N.KF_FMT_FASTQ or (fmt == N.KF_FMT_AUTO and a[0] == ord("@")):
-                fastq = True
-            excl.append(None)
-        ev = torch.cuda.Event()
-        ev.record(stream)
-    if fastq:   # any FASTQ file: the whole batch's record index on the host (from the mappings)
-        maps = iter(reg.maps)
-        full = []
-        for i in range(len(paths)):
-            if sizes[i] == 0:
-                continue
-            a = next(maps)[1]
-            full.append(index_records(a, fmt, int(off[i]))[0])
-        ex = np.concatenate(full) if full else np.zeros(0, np.uint64)
-        return HostBatch(None, off, ex.astype(np.uint64), list(names), dev_data=dev, dev_event=ev, reg=reg)
-    return HostBatch(None, off, None, list(names), dev_data=dev, dev_event=ev, reg=reg)
-
-
 @dataclasses.dataclass
 class DeviceBatch:
     data: torch.Tensor      # uint8 on device (16-byte aligned)
@@ -306,7 +235,7 @@ def to_device(hb: HostBatch, device: torch.device | str = "cuda") -> DeviceBatch
     else:
         data = hb.data.to(dev, non_blocking=True)
     if hb.excl is None:
-        pin = hb.data is None or hb.data.is_pinned()   # data None: registered files copied already
+        pin = hb.data is None or hb.data.is_pinned()
         off = torch.from_numpy(hb.off.view(np.int64))
         off = (off.pin_memory() if pin else off).to(dev, non_blocking=pin)
         with torch.cuda.device(dev):

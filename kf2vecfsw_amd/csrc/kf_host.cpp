@@ -579,6 +579,8 @@ extern "C" int kf_format_kf(const char* name, const uint32_t* counts, uint64_t n
     return KF_OK;
 }
 
+constexpr uint64_t kKeepLineBuf = 16ull << 20;   // a worker's line buffer above this is freed after its item
+
 extern "C" int kf_write_kf_files(const char* dir, const char* const* names, int32_t n, const uint32_t* counts,
                                  uint64_t nbins, int pseudocount, int raw_cnt, int n_threads) {
     if (!dir || (!names && n) || (!counts && n)) return kf_fail(KF_EINVAL, "null argument");
@@ -605,6 +607,10 @@ extern "C" int kf_write_kf_files(const char* dir, const char* const* names, int3
             std::lock_guard<std::mutex> lk(mu);
             if (!err.exchange(1)) errmsg = "cannot write " + path;
         }
+        // the pool's workers never exit: a large-k line buffer (~54 MB at k=11)
+        // is not kept past its item, so a library caller does not hold
+        // threads x 54 MB of host memory after the writes
+        if (buf.capacity() > kKeepLineBuf) std::vector<char>().swap(buf);
     });
     if (err.load()) return kf_fail(KF_EINVAL, "%s", errmsg.c_str());
     return KF_OK;

@@ -95,8 +95,10 @@ constexpr uint32_t kNoOvf = 0xFFFFFFFFu;
 #endif
 // Digit width of the chunk sort's passes (KF_SP_DIGIT = 8 or 10): 10-bit MSD
 // passes sort the top 20 bits, so a 16,384-key chunk over 2^20 values leaves
-// runs of equal top bits for ~1.6 % of its keys instead of ~22 %, and k <= 15
-// chunks are sorted whole in two passes.  64 x 5 Mbp (profiles/r05/v19_*):
+// runs of equal top bits for ~1.6 % of its keys instead of ~22 %, and a chunk
+// whose keys span R = 2k - D + ceil(log2 buckets) <= 20 bits is sorted whole in
+// the two passes (D = 10 bucket bits: k <= 15 for a one-bucket chunk, k <= 14
+// for the usual two to four buckets per chunk).  64 x 5 Mbp (profiles/r05/v19_*):
 // k = 31 7.69 -> 7.23 ms, k = 13 6.37 -> 5.97 (fix-up 0.69e9 -> 0.38e9 cycles,
 // the passes unchanged; 16 KiB of counters per workgroup instead of 4).
 // Phase A loads a workgroup's next tile's bytes while it makes this tile's keys

@@ -155,7 +155,7 @@ def _spawn_shards(argv: list[str], world: int) -> int:
     return max(abs(p.wait()) for p in procs)
 
 
-def visible_gpus() -> int | None:
+def visible_gpus(env=None) -> int | None:
     """GPUs this process may use, counted without initialising HIP (the -gpus
     parent forks children and must never touch the GPU itself): the GPU nodes of
     the KFD topology (nodes with SIMDs), capped by every one of
@@ -176,12 +176,62 @@ def visible_gpus() -> int | None:
     except OSError:
         n_kfd = None
     n = n_kfd
+    env = os.environ if env is None else env
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        v = os.environ.get(var)
+        v = env.get(var)
         if v is not None:
             ids = [x for x in v.split(",") if x.strip() != ""]
             n = len(ids) if n is None else min(n, len(ids))
     return n
+
+
+def usable_cpus() -> tuple[int, dict]:
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2/v1
+    CPU quota if one is set (a GPU box may show the whole host in the mask and
+    in os.cpu_count(), e.g. 256, against a quota of 16)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    return n, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_cpu_quota": quota}
+
+
+def host_threads(p, world: int = 1) -> int:
+    """Host threads of this process (file readers, .kf formatters/writers):
+    min(-p, usable CPUs), split evenly over the `world` processes that share the
+    host (-gpus N children, torchrun ranks on one node).  The reference hands -p
+    to Jellyfish as `-t` (main.py:309) with default mp.cpu_count()
+    (main.py:1031-1033), which on a GPU box counts every host CPU, not the
+    process's quota: 256 threads on a 16-CPU quota."""
+    usable = usable_cpus()[0]
+    return max(1, min(max(1, int(p)), usable) // max(1, int(world)))
+
+
+def _procs_per_host(shard) -> int:
+    """Processes of this run sharing this host's CPUs: the -gpus N children (all
+    local), or torchrun's ranks on this node (LOCAL_WORLD_SIZE)."""
+    if shard is None:
+        return 1
+    if os.environ.get("KF_SHARD"):
+        return shard[1]
+    return int(os.environ.get("LOCAL_WORLD_SIZE", shard[1]))
+
+
+def cli_host_threads(args) -> int:
+    """get_frequencies' host threads in this process: -p capped by the usable
+    CPUs, shared by the processes of this run on this host."""
+    return host_threads(args.p, _procs_per_host(_shard_spec(args)))
 
 
 def get_frequencies(args) -> None:
@@ -236,7 +286,7 @@ def get_frequencies(args) -> None:
             args.k, supported_k.start, supported_k.stop - 1))
 
     import torch
-    from .counter import KmerCounter, pack_files, pack_files_registered, to_device
+    from .counter import KmerCounter, pack_files, to_device
 
     if shard is not None and not os.environ.get("KF_SHARD"):
         # torchrun: join the host-only gloo group now, before counting, so that a
@@ -260,7 +310,7 @@ def get_frequencies(args) -> None:
     # the reference processes files in order and later ones overwrite earlier
     # ones with the same sample name: keep the last occurrence only
     last = {s: i for i, s in enumerate(samples_names)}
-    threads = max(1, int(args.p))
+    threads = cli_host_threads(args)
     from collections import deque
     from concurrent.futures import ThreadPoolExecutor
 
@@ -280,23 +330,12 @@ def get_frequencies(args) -> None:
     # n_slots once the H2D that last read that slot has completed
     slot_bytes = max(sum((os.path.getsize(paths[i]) + 15) // 16 * 16 for i in b) for b in batches)
     n_slots = min(len(batches), int(os.environ.get("KF_READ_AHEAD", "2")) + 2)
-    slots = [torch.empty(max(slot_bytes, 16), dtype=torch.uint8, pin_memory=True)
-             for _ in range(0 if os.environ.get("KF_READ_MODE") == "register" else n_slots)]
+    slots = [torch.empty(max(slot_bytes, 16), dtype=torch.uint8, pin_memory=True) for _ in range(n_slots)]
     slot_ev: list = [None] * n_slots
-
-    # KF_READ_MODE=register: the files' page-cache pages are page-locked in place
-    # and copied by the DMA engine (no host memcpy; counter.pack_files_registered)
-    register = os.environ.get("KF_READ_MODE") == "register"
 
     def pack(bi, idx):
         t0 = now_ms()
         tm = {}
-        if register:
-            hb = pack_files_registered([paths[i] for i in idx], [samples_names[i] for i in idx], device,
-                                       copy_stream)
-            if trace:
-                tr.append(("read", idx[0], t0, now_ms(), tm))
-            return hb
         j = bi % n_slots
         if slot_ev[j] is not None:
             slot_ev[j].synchronize()
@@ -346,13 +385,11 @@ def get_frequencies(args) -> None:
     # pinned count matrix (4 x bins B per genome), so the backlog is bounded
     behind = max(1, int(os.environ.get("KF_WRITE_BEHIND", "2")))
 
-    def write(ev, host, names, reg):
+    def write(ev, host, names):
         ev.synchronize()
-        if reg is not None:   # the batch's copies ran long ago (its count and copy-back have)
-            reg.release()
         t0 = now_ms()
         c = host.numpy().view(np.uint32)
-        write_kf_files(args.output_dir, names, c, args.pseudocount, args.raw_cnt, args.p)
+        write_kf_files(args.output_dir, names, c, args.pseudocount, args.raw_cnt, threads)
         if trace:
             tr.append(("write", names[0] if names else "", t0, now_ms()))
 
@@ -370,7 +407,6 @@ def get_frequencies(args) -> None:
                 e[0].record(stream)
                 evs.append((bi, now_ms(), e))
             db = to_device(hb, device)
-            reg = hb.reg
             del hb
             if trace:
                 e[1].record(stream)
@@ -397,7 +433,7 @@ def get_frequencies(args) -> None:
                 print(">>> Normalizing. Sample: {}".format(files_names[i]))
         if bi >= behind:   # backpressure: at most `behind` batches queued for the writer
             writes[bi - behind].result()
-        writes.append(writer.submit(write, ev, host, [samples_names[idx[j]] for j in keep], reg))
+        writes.append(writer.submit(write, ev, host, [samples_names[idx[j]] for j in keep]))
         del host, rows, counts, db
         if trace:
             th.append(now_ms())
@@ -547,7 +583,7 @@ def get_kmers(args) -> None:
     counter = SparseCounter(args.k, device) if sparse else KmerCounter(args.k, device)
     batch_gb = float(getattr(args, "batch_gb", 4.0) or 4.0)
     budget = int(batch_gb * (1 << 30))
-    if sparse:   # ~25 device bytes per input byte; offsets are 32-bit
+    if sparse:   # ~21 (k <= 16) / ~29 device bytes per input byte with the outputs; 32-bit offsets
         budget = min(budget, 1 << 30)
     # dense k <= 12: the whole count matrix comes back to the host, 4 x bins per
     # genome whatever its size (33.6 MB at k=12): at most -batch_gb of it per batch
@@ -555,7 +591,7 @@ def get_kmers(args) -> None:
     for idx in _batches(fasta_files, budget, max_files=cap):
         paths = [fasta_files[i] for i in idx]
         names = [os.path.basename(p).replace(".fna", "") for p in paths]   # main.py:127
-        hb = pack_files(paths, names)
+        hb = pack_files(paths, names, threads=host_threads(10))   # the reference's `jellyfish count -t 10`
         if sparse:
             keys, cnts, nu = counter.count(to_device(hb, device), int(hb.off[-1]))
             per = counter.to_host(keys, cnts, nu, hb.off)
@@ -635,7 +671,8 @@ def get_chunks(args) -> None:
     # and at most CH.LAUNCH_WINDOWS, so the writer formats one launch while the
     # device counts and copies back the next
     max_windows = max(1, min(budget // CH.CHUNK_SZ, budget // (4 * counter.nbins), CH.LAUNCH_WINDOWS))
-    pipe = CH.ChunkPipeline(counter, device, max_windows, args.p, args.pseudocount)
+    threads = host_threads(args.p)
+    pipe = CH.ChunkPipeline(counter, device, max_windows, threads, args.pseudocount)
     paths = [os.path.join(args.input_dir, f) for f in files_names]
     _refuse_huge_files(paths, "get_chunks (kf_chunk_compact)")
     # input batches of files: about a quarter of the input each (the first two
@@ -644,7 +681,6 @@ def get_chunks(args) -> None:
     # of processed sequence: kf_chunk_compact's offsets)
     total_in = sum(os.path.getsize(p) for p in paths)
     batches = _batches(paths, min(budget, 3 << 30, max(total_in // 4, 16 << 20)), ramp=True)
-    threads = max(1, int(args.p))
     files_pool = ThreadPoolExecutor(max_workers=threads)
     reader = ThreadPoolExecutor(max_workers=1)
 

@@ -6,7 +6,9 @@
   same bytes (OpenMP over the host's CPUs), with and without N runs;
 * configs[3]'s code path -- bench.py's Workload (round-robin shard plan,
   device-generated sub-batches, resident and streamed modes) in-process at a
-  small total, every genome of every sub-batch checked against the oracle.
+  small total, every genome of every sub-batch checked against the oracle --
+  and one rank's full share (6,250 x 5 Mbp, 31.6 GB in one launch) at ranks 0
+  and 7 of 8.
 
 The reference counts with Jellyfish (kf2vec/main.py:309-323); the oracle is its
 restatement pinned by the toy goldens (tests/test_oracle_golden.py)."""
@@ -93,6 +95,53 @@ def test_configs3_shard_path(torch_dev, oracle, resident, rank, world):
     assert m["ok"]
     assert len(m["launch_ms"]) == 2 * W.nsb
     assert m["el"] > 0
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_configs3_rank_share_full_size(torch_dev, oracle, rank):
+    """BASELINE configs[3] at its per-GPU size: rank `rank` of
+    the 8-GPU run owns the 6,250 genome ids g < 50,000 with g mod 8 == rank
+    (6,250 x 5 Mbp = 31.6 GB), generated on the device by bench.py's own Workload
+    and counted at k=7 in ONE kf_count_batch, exactly the launch each rank times.
+    Every total is analytic and every genome's row bit-exact against the oracle
+    on the same bytes, copied back in host chunks of 500 genomes (the host never
+    holds the whole batch).  Reference: the per-file loop this shards,
+    kf2vec/main.py:301-357."""
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    from kf2vecfsw_amd import counter as C
+    args = bench.parse_args(["--workload", "configs3"])
+    W = bench.Workload(args, torch_dev, rank, 8)
+    assert W.nsb == 1 and W.n == 6250 and W.plan == [(rank, 8, 6250)]
+    assert W.fits(7)
+    db = W.gen(0)
+    L, k = args.seq_len, 7
+    assert db.n == 6250 and db.data.numel() > 31.6e9
+    kc = C.KmerCounter(k, torch_dev)
+    cnt, tot = kc.count(db)
+    torch.cuda.synchronize()
+    totals = tot.cpu().numpy()
+    assert (totals == L - k + 1).all()
+    off = db.off.cpu().numpy().view(np.uint64)
+    threads = host_threads()
+    step = 500
+    for g0 in range(0, db.n, step):
+        g1 = min(db.n, g0 + step)
+        host = db.data[int(off[g0]): int(off[g1])].cpu().numpy()
+        if g0 == 0 or g1 == db.n:   # the generator's bytes are the oracle generator's (ids rank + 8 i)
+            for i in (g0, g1 - 1):
+                g = rank + 8 * i
+                exp = oracle.synth_genome(g, SEED + g, L, 80, 0, int(off[i + 1] - off[i]))
+                assert host[int(off[i] - off[g0]): int(off[i + 1] - off[g0])].tobytes() == exp, i
+        oc, ot = oracle.count_many_parts(host, off[g0: g1 + 1] - off[g0], k, 1, threads, 1 << 20)
+        assert np.array_equal(ot, totals[g0:g1]), g0
+        got = C.counts_to_numpy(cnt[g0:g1])
+        bad = np.nonzero((oc != got).any(axis=1))[0]
+        assert bad.size == 0, f"rank {rank}: {bad.size} genomes differ, e.g. {(bad[:8] + g0).tolist()}"
+        del host, oc, got
+    del cnt, tot, db
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("n_period", [0, 3])

@@ -42,3 +42,35 @@ def test_refuse_huge_files(tmp_path):
     with pytest.raises(ValueError, match="huge.fna"):
         M._refuse_huge_files([str(small), str(huge)], "get_kmers -k 21")
     os.remove(huge)
+
+
+@pytest.mark.parametrize("world,expect", [(1, 16), (2, 8), (8, 2)])
+def test_cli_host_threads_split_under_quota(monkeypatch, world, expect):
+    """-p defaults to mp.cpu_count() (main.py:1031-1033),
+    which on the GPU box is 256 against a 16-CPU cgroup quota.  Each process of a
+    run gets min(-p, usable CPUs) split over the processes on the host: a -gpus N
+    child (KF_SHARD "r,N"), a torchrun rank (LOCAL_WORLD_SIZE), or the single
+    process (faked 16-CPU quota here)."""
+    import argparse
+    monkeypatch.setattr(M, "usable_cpus", lambda: (16, {"cgroup_cpu_quota": 16.0}))
+    monkeypatch.setattr(M.mp, "cpu_count", lambda: 256)          # the box's nproc: -p's default and choices
+    for var in ("KF_SHARD", "WORLD_SIZE", "RANK", "LOCAL_WORLD_SIZE"):
+        monkeypatch.delenv(var, raising=False)
+    args = argparse.Namespace(p=M.build_parser().parse_args(["get_frequencies"]).p, gpus=1)
+    assert args.p == 256
+    if world == 1:
+        assert M.cli_host_threads(args) == expect
+    for r in range(world):                        # every -gpus N child (its parent passes -p through)
+        monkeypatch.setenv("KF_SHARD", f"{r},{world}")
+        child = M.build_parser().parse_args(
+            M._child_argv(argparse.Namespace(input_dir="i", output_dir="o", k=7, p=256, pseudocount=False,
+                                             raw_cnt=False, batch_gb=None)))
+        assert child.p == 256 and M.cli_host_threads(child) == expect
+    monkeypatch.delenv("KF_SHARD")
+    monkeypatch.setenv("WORLD_SIZE", str(world))   # torchrun ranks on one node
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", str(world))
+    for r in range(world):
+        monkeypatch.setenv("RANK", str(r))
+        assert M.cli_host_threads(args) == expect
+    # -p below the quota is honoured, and a process never gets 0 threads
+    assert M.host_threads(4, 1) == 4 and M.host_threads(4, 8) == 1 and M.host_threads(1, 16) == 1
