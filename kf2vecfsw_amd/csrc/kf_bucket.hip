@@ -1129,20 +1129,16 @@ int bucket_launch_info(int k, int* grid, int* block, int* lds) {
 // for the largest compiled geometry, so every k shares it) and a piece table of
 // at least n_genomes+1 words (grown 2x at a time; a regrowth synchronises the
 // device, since a launch in flight may still read the old one).
+int ensure_scratch(DevState& d, int dev, size_t need);
+
 int ensure_workspace(DevState& d, int dev, int k, int32_t n_genomes) {
     void* fn = bucket_kernel_for(k);
     if (!fn) return kf_fail(KF_EINVAL, "no bucket kernel for k=%d", k);
     const uint32_t lds = bucket_lds_for(k);
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    if (!d.cus) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return kf_fail(KF_EHIP, "hipDeviceGetAttribute(MultiprocessorCount) failed");
-        d.cus = cus > 0 ? cus : 1;
-        if (hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess)
-            return kf_fail(KF_EHIP, "hipEventCreate failed");
-    }
+    int rc0 = ensure_scratch(d, dev, 0);   // the device state
+    if (rc0) return rc0;
     size_t rec_b = 0, meta_b = 0, roff_b = 0;
     scratch_layout(d.cus, rec_b, meta_b, roff_b);
     const size_t need = rec_b + meta_b + roff_b;
@@ -1152,19 +1148,8 @@ int ensure_workspace(DevState& d, int dev, int k, int32_t n_genomes) {
         if (rc) return rc;
     }
 #endif
-    if (d.scratch_bytes < need) {
-        if (d.scratch && (hipDeviceSynchronize() != hipSuccess || hipFree(d.scratch) != hipSuccess))
-            return kf_fail(KF_EHIP, "hipFree of bucket scratch failed");
-        d.scratch = nullptr;
-        d.scratch_bytes = 0;
-#ifdef KF_PROFILE_BUILD
-        // profiling builds: KF_BUCKET_CONTIG=1 asks for physically contiguous scratch
-        if (!(getenv("KF_BUCKET_CONTIG") && hipExtMallocWithFlags(&d.scratch, need, hipDeviceMallocContiguous) == hipSuccess))
-#endif
-        if (hipMalloc(&d.scratch, need) != hipSuccess)
-            return kf_fail(KF_EHIP, "hipMalloc of %zu bytes of bucket scratch failed", need);
-        d.scratch_bytes = need;
-    }
+    rc0 = ensure_scratch(d, dev, need);
+    if (rc0) return rc0;
     // the tables after the scratch (KF_BUCKET_TABLES_FIRST=1, profiling builds:
     // before it, the order of rounds 2-4)
 #ifdef KF_PROFILE_BUILD
@@ -1191,6 +1176,57 @@ int ensure_workspace(DevState& d, int dev, int k, int32_t n_genomes) {
             return kf_fail(KF_EHIP, "hipMalloc of piece table failed");
         d.pstart_n = cap;
     }
+    return KF_OK;
+}
+
+// The device state (CU count, the scratch's event) and a scratch of at least
+// `need` bytes (caller holds g_mu).
+int ensure_scratch(DevState& d, int dev, size_t need) {
+    if (!d.cus) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipDeviceGetAttribute(MultiprocessorCount) failed");
+        d.cus = cus > 0 ? cus : 1;
+        if (hipEventCreateWithFlags(&d.done, hipEventDisableTiming) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipEventCreate failed");
+    }
+    if (d.scratch_bytes < need) {
+        if (d.scratch && (hipDeviceSynchronize() != hipSuccess || hipFree(d.scratch) != hipSuccess))
+            return kf_fail(KF_EHIP, "hipFree of bucket scratch failed");
+        d.scratch = nullptr;
+        d.scratch_bytes = 0;
+#ifdef KF_PROFILE_BUILD
+        // profiling builds: KF_BUCKET_CONTIG=1 asks for physically contiguous scratch
+        if (!(getenv("KF_BUCKET_CONTIG") && hipExtMallocWithFlags(&d.scratch, need, hipDeviceMallocContiguous) == hipSuccess))
+#endif
+        if (hipMalloc(&d.scratch, need) != hipSuccess)
+            return kf_fail(KF_EHIP, "hipMalloc of %zu bytes of bucket scratch failed", need);
+        d.scratch_bytes = need;
+    }
+    return KF_OK;
+}
+
+int scratch_reserve(size_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
+    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_mu);
+    return ensure_scratch(g_dev[dev], dev, bytes);
+}
+
+int scratch_launch(size_t bytes, hipStream_t s, const std::function<int(void*)>& launch) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
+    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevState& d = g_dev[dev];
+    int rc = ensure_scratch(d, dev, bytes);
+    if (rc) return rc;
+    if (d.done && hipStreamWaitEvent(s, d.done, 0) != hipSuccess)
+        return kf_fail(KF_EHIP, "hipStreamWaitEvent failed");
+    rc = launch(d.scratch);
+    if (rc) return rc;
+    if (hipEventRecord(d.done, s) != hipSuccess) return kf_fail(KF_EHIP, "hipEventRecord failed");
     return KF_OK;
 }
 

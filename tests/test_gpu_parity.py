@@ -481,8 +481,8 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, k):
     """k=7 K1x: its u16 LDS counters overflow on low-complexity sequence unless the
     drain path moves counts out exactly (poly-A, dinucleotide and satellite
     repeats, N-broken poly-A that fills the unpaired-window table, and FASTA lines
-    of 1-7 bases that keep every iteration on the irregular path).  k=9: the
-    bucket kernel on the same inputs, where one bucket takes almost every record."""
+    of 1-7 bases that keep every iteration on the irregular path).  k=9: K9s on
+    the same inputs (poly-A's class is in part 0: phase-1 drains)."""
     rng = np.random.default_rng(4242)
     sat = gen.random_seq(rng, 171).tobytes()
     polya = b"A" * 40_000_000
@@ -501,6 +501,71 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, k):
              for _ in range(300)]
     counts, totals = run_batch(blobs, k, torch_dev)
     check_against_oracle(oracle, blobs, k, counts, totals, tag="u16-many")
+
+
+def _k9_part1_walk(rng, n):
+    """A sequence whose 9-mers are mostly in K9s's part 1 (class first base T or
+    G): each next base is drawn among those that keep the window in part 1 when
+    any does (about 2/3 of the windows end up there)."""
+    y = np.arange(1 << 18, dtype=np.uint32)   # kf code A0 C1 T2 G3
+    rc, t = np.zeros_like(y), y.copy()
+    for _ in range(9):
+        rc, t = (rc << 2) | ((t & 3) ^ 2), t >> 2
+    part = ((np.where((y >> 9) & 1, rc, y) >> 17) & 1).reshape(-1, 4)
+    seq = np.empty(n, np.uint8)
+    ctx = 0
+    for i in range(n):
+        opts = np.nonzero(part[ctx])[0] if i >= 8 else np.arange(4)
+        b = int(rng.choice(opts)) if len(opts) else int(rng.integers(4))
+        seq[i] = b
+        ctx = ((ctx << 2) | b) & 0xFFFF
+    return np.frombuffer(b"ACTG", np.uint8)[seq]
+
+
+def test_k9_staged_part1_heavy_and_periodic(torch_dev, oracle):
+    """K9s (k = 9, one pass): part-1-heavy sequence (regions with more than 512
+    staged records: two copy-out rounds), short lines and records (the irregular
+    path stages too), and periodic sequence whose few classes overflow the u16
+    halves in both phases (phase-1 and phase-2 drains, and the padding records'
+    class 0xFFFF of part 1 = GGGGAGGGG... mixed in).  kf2vec/main.py:293-294."""
+    rng = np.random.default_rng(909)
+    walk = _k9_part1_walk(rng, 400_000)
+    blobs = [b">w\n" + gen.wrap(walk, 80),
+             b">w60\n" + gen.wrap(walk[:123_457], 60) + b">w2\n" + gen.wrap(walk[200_000:], 7),
+             b"".join(b">r%d\n" % i + gen.wrap(walk[i * 3000: i * 3000 + 2500], 61) for i in range(40))]
+    for unit in (b"TG", b"TTA", b"TTTTA", b"GGGGAGG", b"TGCA", b"GATTACA"):
+        blobs.append(b">p\n" + gen.wrap(np.frombuffer(unit * (3_000_000 // len(unit)), np.uint8), 80))
+    blobs.append(b">g\n" + gen.wrap(np.frombuffer(b"GGGGAGGGG" * 400_000, np.uint8), 80))
+    counts, totals = run_batch(blobs, 9, torch_dev)
+    check_against_oracle(oracle, blobs, 9, counts, totals, tag="k9s")
+
+
+def test_k9_two_segments_every_genome(torch_dev, oracle):
+    """K9s splits a batch into G x ceil(total / (G x 20 MiB)) segments: 1,200 x 5
+    Mbp (6.07 GB, N runs) gives every workgroup two, so its record scratch is
+    reused and genomes straddle segment boundaries (atomic flushes).  Every
+    genome's row and total bit-exact against the oracle."""
+    import torch
+    from kf2vecfsw_amd import counter as C
+    from test_gpu_configs import host_threads
+    n, L, k = 1200, 5_000_000, 9
+    db = C.synth_device_batch(n, L, 20260101, width=80, n_period=3, device=torch_dev)
+    assert int(db.off[-1]) > 256 * (20 << 20)
+    cnt, tot = counter(k, torch_dev).count(db)
+    torch.cuda.synchronize()
+    totals = tot.cpu().numpy()
+    off = db.off.cpu().numpy().view(np.uint64)
+    threads = host_threads()
+    for g0 in range(0, n, 200):
+        g1 = min(n, g0 + 200)
+        host = db.data[int(off[g0]): int(off[g1])].cpu().numpy()
+        oc, ot = oracle.count_many_parts(host, off[g0: g1 + 1] - off[g0], k, 1, threads, 1 << 20)
+        assert np.array_equal(ot, totals[g0:g1]), g0
+        got = C.counts_to_numpy(cnt[g0:g1])
+        bad = np.nonzero((oc != got).any(axis=1))[0]
+        assert bad.size == 0, f"k=9: {bad.size} genomes differ, e.g. {(bad[:8] + g0).tolist()}"
+    del cnt, tot, db
+    torch.cuda.empty_cache()
 
 
 def test_k7_many_pieces_many_records(torch_dev, oracle):
