@@ -56,7 +56,9 @@ def _stale() -> bool:
 
 def build(force: bool = False, verbose: bool = False, ablation: bool = False, out: str | None = None) -> str:
     """ablation=True: a profiling build of the product (KF_PROFILE_BUILD: the
-    bucket kernels' KF_BUCKET_PROFILE / KF_BK_WEIGHTS knobs).
+    bucket kernels' KF_BUCKET_PROFILE / KF_BK_WEIGHTS knobs, KF_K9_BUCKET) from
+    the sources with tools/zoo/bucket_ablations.patch applied (KF_BK_ABL=n via
+    KF_HIPCC_FLAGS).
     Serialised by a file lock: every rank of a multi-process run may call it."""
     import fcntl
     out = out or OUT
@@ -90,20 +92,38 @@ def _toolchain_id() -> bytes:
     return _TOOLCHAIN[0]
 
 
-def _object(src: str, cmd_tail: list[str]) -> tuple[str, bool]:
+def _object(src: str, cmd_tail: list[str], csrc: str = CSRC) -> tuple[str, bool]:
     """Object path for `src` compiled with `cmd_tail`, keyed by the hash of the
     source, the shared headers, the command and the compilers' versions (so an
     edit rebuilds only the objects it touches); and whether it already exists."""
     h = hashlib.sha256(" ".join(cmd_tail).encode() + b"\0" + _toolchain_id())
     for d in [src] + HEADERS:
-        with open(os.path.join(CSRC, d), "rb") as f:
+        with open(os.path.join(csrc, d), "rb") as f:
             h.update(f.read())
     o = os.path.join(BUILD, f"{src}.{h.hexdigest()[:16]}.o")
     return o, os.path.exists(o)
 
 
+ABL_PATCH = os.path.join(HERE, "..", "tools", "zoo", "bucket_ablations.patch")
+
+
+def _ablation_sources() -> str:
+    """A copy of csrc/ (and the header) with tools/zoo/bucket_ablations.patch
+    applied: the bucket kernels' KF_BK_ABL=n profiling ablations (wrong counts by
+    design), kept out of the product source.  Returns its csrc directory."""
+    import shutil
+    root = os.path.join(BUILD, "abl_src")
+    shutil.rmtree(root, ignore_errors=True)
+    shutil.copytree(CSRC, os.path.join(root, "kf2vecfsw_amd", "csrc"))
+    os.makedirs(os.path.join(root, "include"))
+    shutil.copy(os.path.join(HERE, "..", "include", "kf2vec_gpu.h"), os.path.join(root, "include"))
+    subprocess.run(["patch", "-s", "-p1", "-d", root, "-i", os.path.abspath(ABL_PATCH)], check=True)
+    return os.path.join(root, "kf2vecfsw_amd", "csrc")
+
+
 def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
     objs = []
+    csrc = _ablation_sources() if ablation else CSRC
     # profiling / ablation builds carry a suffix, so the product check refuses them
     flags = os.environ.get("KF_HIPCC_FLAGS", "")
     bid = source_id() + ("+prof" if ablation else "") + \
@@ -111,9 +131,9 @@ def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
     for s in SOURCES_HIP:
         tail = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"] + \
             (["-DKF_PROFILE_BUILD"] if ablation else []) + flags.split()   # KF_HIPCC_FLAGS: tools/ only
-        o, have = _object(s, tail)
+        o, have = _object(s, tail, csrc)
         if not have or verbose:
-            cmd = [HIPCC] + tail + ["-c", os.path.join(CSRC, s), "-o", o + ".tmp"]
+            cmd = [HIPCC] + tail + ["-c", os.path.join(csrc, s), "-o", o + ".tmp"]
             if verbose:
                 cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
             subprocess.run(cmd, check=True)
@@ -121,9 +141,9 @@ def _build_locked(verbose: bool, ablation: bool, out: str) -> str:
         objs.append(o)
     for s in SOURCES_CPP:
         tail = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-pthread", f'-DKF_BUILD_ID="{bid}"']
-        o, have = _object(s, tail)
+        o, have = _object(s, tail, csrc)
         if not have:
-            subprocess.run(["g++"] + tail + ["-c", os.path.join(CSRC, s), "-o", o + ".tmp"], check=True)
+            subprocess.run(["g++"] + tail + ["-c", os.path.join(csrc, s), "-o", o + ".tmp"], check=True)
             os.replace(o + ".tmp", o)
         objs.append(o)
     tmp = out + ".tmp"

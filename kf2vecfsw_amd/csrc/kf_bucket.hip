@@ -33,17 +33,9 @@
 
 namespace kf {
 
-// Profiling-only ablations (-DKF_BK_ABL=n through KF_HIPCC_FLAGS; counts are
-// wrong): 1 = no col_idx table reads in the flush, 2 = no record reads in phase
-// 2 (hashed stand-ins), 3 = no phase-1 rank atomics (dense path; the round counts
-// stay 0, so no records are written or read at all), 4 = no
-// phase-1 staging writes (dense path), 5 = no phase-2 histogram adds, 7 = rank
-// adds without returns, 8 = no phase 2 (rows stay zero), 9 = as 1 with
-// lane-consecutive flush slots (no LDS bank conflicts in the flush), 10 = no
-// barrier after each bucket's flush, 11 = no phase-2 barriers.
-#ifndef KF_BK_ABL
-#define KF_BK_ABL 0
-#endif
+// (The profiling ablations of rounds 3-5 -- wrong counts by design -- live in
+// tools/zoo/bucket_ablations.patch, applied by `python -m kf2vecfsw_amd.build
+// --ablation`; DESIGN.md section 4 lists them.)
 // Phase 2 record groups: 1 = two groups of 4 windows alternate (the next one in
 // flight while one is counted), 0 = one group of 8 windows (a bucket's further
 // groups wait for their loads).
@@ -516,16 +508,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
                     carry = w.next;
                     canon_std<K, true>(w, s);
 #pragma unroll
-#if KF_BK_ABL == 3   // profiling only: no rank atomics (ranks by lane: wrong counts)
-                    for (int j = 0; j < 15; ++j) rk[j] = (uint32_t)lane * 16 + j;
-#elif KF_BK_ABL == 7   // profiling only: rank adds without returns (ranks by lane: wrong counts)
-                    for (int j = 0; j < 15; ++j) {
-                        lds_add(cbr | ent_b(s[j]), 1u);
-                        rk[j] = (uint32_t)lane * 16 + j;
-                    }
-#else
                     for (int j = 0; j < 15; ++j) rk[j] = lds_add_rtn(cbr | ent_b(s[j]), 1u);
-#endif
                     if (s[15] != 0xFFFFFFFFu) rk[15] = lds_add_rtn(cbr | ent_b(s[15]), 1u);
                 } else {
                     uint32_t C, V, EN, ne, own;
@@ -654,11 +637,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
                 if (s[15] != 0xFFFFFFFFu) rk[15] += lds_ld(rbr + ent_b(s[15]));
 #pragma unroll
                 for (int j = 0; j < 15; ++j) {
-#if KF_BK_ABL == 4   // profiling only: no staging writes (wrong counts)
-                    asm volatile("" ::"v"(rk[j]), "v"(s[j]));
-#else
                     *(volatile lds_u16*)(uintptr_t)(st + 2 * stage_slot(rk[j])) = (uint16_t)s[j];
-#endif
                 }
                 if (s[15] != 0xFFFFFFFFu)
                     *(volatile lds_u16*)(uintptr_t)(st + 2 * stage_slot(rk[15])) = (uint16_t)s[15];
@@ -806,12 +785,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
                 const bool a = u < t.U;
                 G.act |= a ? 1u << x : 0u;
                 const uint32_t q = a ? 8 * (u + dl) : 0u;
-                if (KF_BK_ABL == 2) {
-                    const uint32_t h = q * 2654435761u;
-                    G.v[x] = v4u{h, h * 2246822519u, h * 3266489917u, h * 668265263u} & 0x7FFF7FFFu;
-                } else {
-                    G.v[x] = __builtin_nontemporal_load((const v4u*)(rec + q));
-                }
+                G.v[x] = __builtin_nontemporal_load((const v4u*)(rec + q));
             }
             t.w0 += kGW * kWave;
         };
@@ -821,12 +795,8 @@ bucket_kernel(CountArgs A, BucketArgs B) {
                 if (G.w0 + x * kWave >= U) break;   // wave-uniform
                 if (G.act & (1u << x)) {
                     const uint32_t d[4] = {G.v[x].x ^ pm, G.v[x].y ^ pm, G.v[x].z ^ pm, G.v[x].w ^ pm};
-#if KF_BK_ABL == 5   // profiling only: phase 2 without its histogram adds (wrong counts)
-                    asm volatile("" ::"v"(d[0]), "v"(d[1]), "v"(d[2]), "v"(d[3]));
-#else
 #pragma unroll
                     for (int t = 0; t < 8; ++t) lds_add(rec_addr(d[t >> 1], t & 1), 1u);
-#endif
                 }
             }
         };
@@ -838,14 +808,6 @@ bucket_kernel(CountArgs A, BucketArgs B) {
         constexpr int kFG = 8;
         typedef unsigned int v2u __attribute__((ext_vector_type(2)));
         auto col_at = [&](uint32_t g4) -> v2u {
-            if (KF_BK_ABL == 1) {
-                const uint32_t x = (2 * g4) & (L::codes - 4u);
-                return v2u{x | (x + 1) << 16, (x + 2) | (x + 3) << 16};
-            }
-            if (KF_BK_ABL == 9) {   // no col_idx reads and lane-consecutive slots (no bank conflicts)
-                const uint32_t m = L::codes - 1u, x = (g4 >> 2) & m;
-                return v2u{x | ((x + 1024u) & m) << 16, ((x + 2048u) & m) | ((x + 3072u) & m) << 16};
-            }
             return *(const v2u*)(B.col_idx + g4);
         };
         // c0, c1: the bucket's column range, loaded here (before the next bucket's
@@ -907,7 +869,7 @@ bucket_kernel(CountArgs A, BucketArgs B) {
 #endif
         uint64_t tp[4] = {0, 0, 0, 0};   // profile: records, barrier, flush, barrier
         uint64_t tcons = 0;              // profile: consume part of records
-        for (uint32_t b = 0; b < (KF_BK_ABL == 8 ? 0u : NBK); ++b) {   // (ABL 8: phase 1 only)
+        for (uint32_t b = 0; b < NBK; ++b) {
             uint64_t t0 = B.prof ? __builtin_amdgcn_s_memtime() : 0;
             const uint32_t pm = ((b & L::hmask) << L::bits) * 0x10001u;   // both records of a word
 #if KF_BK_DB
@@ -959,18 +921,14 @@ bucket_kernel(CountArgs A, BucketArgs B) {
             }
             re_next = m;
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[0] += t - t0; t0 = t; }
-#if KF_BK_ABL != 11   // profiling only (11: no phase-2 barriers at all; wrong counts)
             lds_barrier();
-#endif
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[1] += t - t0; t0 = t; }
 #pragma unroll
             for (int x = 0; x < kFG; ++x) flush_cols((c0 & ~3u) + 4 * ((uint32_t)tid + x * L::block), ci[x], c0, c1);
             for (uint32_t g4 = (c0 & ~3u) + 4 * ((uint32_t)tid + kFG * L::block); g4 < c1; g4 += 4 * L::block)
                 flush_cols(g4, col_at(g4), c0, c1);
             if (B.prof) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const uint64_t t = __builtin_amdgcn_s_memtime(); tp[2] += t - t0; t0 = t; }
-#if KF_BK_ABL != 10 && KF_BK_ABL != 11   // profiling only (10: no barrier after the flush, the
-            lds_barrier();                     // bound of overlapping a flush with the next count)
-#endif
+            lds_barrier();
             if (B.prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); tp[3] += t - t0; }
         }
         if (B.prof && lane == 0) {   // per wave: records, barrier, (phase-1 barrier), consume
