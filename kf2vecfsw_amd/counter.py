@@ -186,6 +186,42 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
     return HostBatch(data, off, ex.astype(np.uint64), list(names) if names else list(paths))
 
 
+def pack_ranges(ranges: Sequence[tuple[str, int, int]], names: Sequence[str] | None = None, pin: bool = True,
+                threads: int = 8, chunk: int = 64 << 20) -> HostBatch:
+    """As pack_files for byte ranges [(path, start, end)] of files (the pieces of
+    a file too large for one sparse call, main.fasta_pieces), read by os.preadv
+    in chunks of `chunk` bytes on `threads` threads; FASTA only (the record index
+    is left to the device)."""
+    from concurrent.futures import ThreadPoolExecutor
+    sizes = [e - a for _, a, e in ranges]
+    off = _layout(sizes)
+    data = _alloc_host(int(off[-1]), pin)
+    d = data.numpy()
+    d[: int(off[-1])] = 10                       # '\n' padding is transparent
+    jobs = []
+    for i, (p, a, e) in enumerate(ranges):
+        for x in range(a, e, chunk):
+            jobs.append((p, x, min(e, x + chunk), int(off[i]) + x - a))
+
+    def read(job):
+        p, x, y, dst = job
+        fd = os.open(p, os.O_RDONLY)
+        try:
+            got = 0
+            mv = memoryview(d[dst: dst + (y - x)])
+            while got < y - x:
+                r = os.preadv(fd, [mv[got:]], x + got)
+                if r <= 0:
+                    raise N.NativeError(f"short read on {p}")
+                got += r
+        finally:
+            os.close(fd)
+
+    with ThreadPoolExecutor(max_workers=max(1, int(threads))) as ex:
+        list(ex.map(read, jobs))
+    return HostBatch(data, off, None, list(names) if names else [f"{p}:{a}" for p, a, _ in ranges])
+
+
 @dataclasses.dataclass
 class DeviceBatch:
     data: torch.Tensor      # uint8 on device (16-byte aligned)

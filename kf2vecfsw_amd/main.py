@@ -561,15 +561,114 @@ def _refuse_huge_files(paths: list[str], what: str) -> None:
             what, ", ".join(os.path.basename(p) for p in big[:5])))
 
 
+SPLIT_BYTES = 1 << 30   # get_kmers' sparse path: FASTA files above this are counted in pieces
+
+
+def _line_start(f, pos: int) -> int:
+    """Offset of the first byte of the line holding byte `pos`."""
+    step = 1 << 16
+    hi = pos
+    while hi > 0:
+        lo = max(0, hi - step)
+        blk = os.pread(f, hi - lo, lo)
+        j = blk.rfind(b"\n")
+        if j >= 0:
+            return lo + j + 1
+        hi = lo
+    return 0
+
+
+def _overlap_start(fd: int, s: int, k: int) -> int:
+    """The byte where a piece whose windows end at or after s must start: k-1
+    sequence positions before s (newlines are transparent, every other byte is a
+    position), or just after a header line, or the file start."""
+    w = 1 << 12
+    while True:
+        lo = max(0, s - w)
+        blk = os.pread(fd, s - lo, lo)
+        need, q, o, short = k - 1, len(blk), s, False
+        while q > 0 and need > 0:
+            q -= 1
+            if blk[q] == 10:                          # into the line before: a header ends the walk
+                ls = blk.rfind(b"\n", 0, q) + 1
+                if ls == 0 and lo > 0:
+                    short = True
+                    break
+                if blk[ls: ls + 1] == b">":
+                    return lo + q + 1
+                continue
+            need -= 1
+            o = lo + q
+        if not short and (need == 0 or lo == 0):
+            o = 0 if need > 0 else o
+            if o < s and os.pread(fd, 1, o) == b">":   # a '>' inside a line must not start a piece
+                o -= 1                                 # (the device index would take it for a header)
+            return o
+        w <<= 2
+
+
+def fasta_pieces(path: str, k: int, piece: int = SPLIT_BYTES) -> list[tuple[int, int]]:
+    """Byte ranges [(o_i, e_i)] that count a large FASTA file in pieces (each below
+    the sparse counter's 32-bit offsets) with every window counted exactly once.
+    Piece i owns the windows ending in [s_i, s_{i+1}) (s_0 = 0, the last ends at
+    the file end; a cut s_i lies on a sequence line, moved past a header line).
+    Its bytes start k-1 sequence positions earlier, at o_i (_overlap_start):
+    fewer than k positions before s_i, so no window ends there, and every window
+    ending at or after s_i has its context.  Windows never span a header, so
+    pieces never need more.  Jellyfish counts a file of any size in one hash
+    (kf2vec/main.py:133-145); this is the device counter's way there."""
+    size = os.path.getsize(path)
+    if size <= piece:
+        return [(0, size)]
+    cuts = [0]
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        for i in range(1, -(-size // piece)):
+            s = i * piece
+            ls = _line_start(fd, s)
+            if os.pread(fd, 1, ls) == b">":           # a header line: cut after it
+                rest = s
+                while True:
+                    blk = os.pread(fd, 1 << 16, rest)
+                    j = blk.find(b"\n")
+                    if j >= 0 or not blk:
+                        s = rest + (j + 1 if j >= 0 else len(blk))
+                        break
+                    rest += len(blk)
+            if s >= size or s <= cuts[-1]:
+                continue
+            cuts.append(s)
+        return [(_overlap_start(fd, c, k) if c else 0, cuts[i + 1] if i + 1 < len(cuts) else size)
+                for i, c in enumerate(cuts)]
+    finally:
+        os.close(fd)
+
+
+def _merge_sorted_counts(parts: list) -> tuple:
+    """Union of per-piece (keys int64, counts) device tensors with equal keys'
+    counts summed (int64: a merged count may pass 2^32); keys ascending."""
+    import torch
+    keys = torch.cat([p[0] for p in parts])
+    cnts = torch.cat([p[1].to(torch.int64) & 0xFFFFFFFF for p in parts])
+    if keys.numel() == 0:
+        return keys, cnts
+    ks, order = torch.sort(keys)
+    u, inv = torch.unique_consecutive(ks, return_inverse=True)
+    out = torch.zeros(u.numel(), dtype=torch.int64, device=keys.device).index_add_(0, inv, cnts[order])
+    return u, out
+
+
 def get_kmers(args) -> None:
     """kf2vec/main.py:112-184 on the GPU (the *.fna of input_dir in batches).
     k <= 12: the dense counter's rows, non-zero bins kept; k = 13..31 (the rest
     of the reference's 2..31): the sparse counter (device radix sort of every
-    window's canonical code, kf_sparse_count)."""
+    window's canonical code, kf_sparse_count); a FASTA file above SPLIT_BYTES
+    goes through it in pieces (fasta_pieces) whose sorted results are merged on
+    the device, so no file size is refused."""
     import glob
 
     import torch
-    from .counter import KmerCounter, SparseCounter, counts_to_numpy, pack_files, to_device
+    from .counter import KmerCounter, SparseCounter, counts_to_numpy, pack_files, pack_ranges, to_device
 
     if not os.path.exists(args.output_dir):             # main.py:121-122
         os.makedirs(args.output_dir)
@@ -578,8 +677,9 @@ def get_kmers(args) -> None:
         return
     device = torch.device(getattr(args, "device", None) or "cuda")
     sparse = args.k > N.KF_MAX_K
-    if sparse:
-        _refuse_huge_files(fasta_files, "get_kmers -k {} (kf_sparse_count)".format(args.k))
+    if sparse:   # FASTQ content (first byte '@') is not cut: its record state does not split
+        fq = [p for p in fasta_files if os.path.getsize(p) > SPLIT_BYTES and open(p, "rb").read(1) == b"@"]
+        _refuse_huge_files(fq, "get_kmers -k {} (kf_sparse_count, FASTQ content)".format(args.k))
     counter = SparseCounter(args.k, device) if sparse else KmerCounter(args.k, device)
     batch_gb = float(getattr(args, "batch_gb", 4.0) or 4.0)
     budget = int(batch_gb * (1 << 30))
@@ -588,6 +688,9 @@ def get_kmers(args) -> None:
     # dense k <= 12: the whole count matrix comes back to the host, 4 x bins per
     # genome whatever its size (33.6 MB at k=12): at most -batch_gb of it per batch
     cap = None if sparse else _count_cap(4 * counter.nbins, batch_gb)
+    if sparse and any(os.path.getsize(p) > SPLIT_BYTES for p in fasta_files):
+        _get_kmers_pieces(args, fasta_files, counter, device, budget)
+        return
     for idx in _batches(fasta_files, budget, max_files=cap):
         paths = [fasta_files[i] for i in idx]
         names = [os.path.basename(p).replace(".fna", "") for p in paths]   # main.py:127
@@ -608,6 +711,63 @@ def get_kmers(args) -> None:
             output_path = os.path.join(args.output_dir, f"{base_name}_k{args.k}.npy")
             np.save(output_path, m)
             print(f"Saved: {output_path} (Shape: {m.shape})")
+
+
+def _get_kmers_pieces(args, fasta_files: list[str], counter, device, budget: int) -> None:
+    """get_kmers' sparse path with files above SPLIT_BYTES: every file as its
+    fasta_pieces, the pieces in batches of at most `budget` bytes, a file's
+    piece results kept on the device until its last piece is counted, then
+    merged (_merge_sorted_counts) and written as main.py:147-176 does."""
+    import torch
+    from .counter import pack_ranges, to_device
+    units = []                                    # (file index, start, end)
+    for fi, p in enumerate(fasta_files):
+        for a, e in fasta_pieces(p, args.k):
+            units.append((fi, a, e))
+    last = {fi: j for j, (fi, _, _) in enumerate(units)}
+    pending: dict = {}
+    batch, size = [], 0
+
+    def run(batch):
+        hb = pack_ranges([(fasta_files[fi], a, e) for fi, a, e in batch], threads=host_threads(10))
+        db = to_device(hb, device)
+        keys, cnts, nu = counter.count(db, int(hb.off[-1]))
+        nuh = nu.cpu().numpy()
+        if nuh.size and ((nuh == -1).any() or (nuh == -2).any()):
+            counter.to_host(keys, cnts, nu, hb.off)   # raises the library's error
+        for j, (fi, _, _) in enumerate(batch):
+            lo, m = int(hb.off[j]), int(nuh[j])
+            pending.setdefault(fi, []).append((keys[lo: lo + m].clone(), cnts[lo: lo + m].clone()))
+        del keys, cnts, nu, db, hb
+
+    def finish(fi):
+        k_, c_ = _merge_sorted_counts(pending.pop(fi))
+        base_name = os.path.basename(fasta_files[fi]).replace(".fna", "")   # main.py:127
+        print(f"--- Processing {base_name} ---")
+        m = sparse_kmers_matrix(k_.cpu().numpy().view(np.uint64), c_.cpu().numpy(), args.k)
+        if m.shape[0] == 0:
+            print(f"Warning: No valid ATCG k-mers found in {base_name}")
+            return
+        output_path = os.path.join(args.output_dir, f"{base_name}_k{args.k}.npy")
+        np.save(output_path, m)
+        print(f"Saved: {output_path} (Shape: {m.shape})")
+
+    done = 0
+    for j, u in enumerate(units):
+        n = u[2] - u[1]
+        if batch and size + n > budget:
+            run(batch)
+            batch, size = [], 0
+            while done < len(fasta_files) and last[done] < j:
+                finish(done)
+                done += 1
+        batch.append(u)
+        size += (n + 15) // 16 * 16
+    if batch:
+        run(batch)
+    while done < len(fasta_files):
+        finish(done)
+        done += 1
 
 
 # ---------------------------------------------------------------------------

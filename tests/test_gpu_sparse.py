@@ -208,3 +208,60 @@ def test_sparse_rejects_bad_offsets(torch_dev):
     keys, cnts, nu = sc.count(db2, int(hb.off[-1]) + 64)
     torch.cuda.synchronize()
     assert (nu.cpu().numpy() == -1).all()
+
+
+def _combine(terms):
+    """sum of coef x (keys, counts) sparse vectors -> sorted keys, int64 counts (zeros dropped)."""
+    keys = np.unique(np.concatenate([t[1] for t in terms]))
+    acc = np.zeros(keys.size, np.int64)
+    for coef, k_, c_ in terms:
+        acc[np.searchsorted(keys, k_)] += coef * c_.astype(np.int64)
+    nz = acc != 0
+    return keys[nz], acc[nz]
+
+
+def test_get_kmers_5gib_file_in_pieces(torch_dev, oracle, tmp_path):
+    """get_kmers -k 21 on ONE ~5 GiB FASTA (a 4.7 Gbp record,
+    far past the sparse counter's 4 GiB per call, then a 0.3 Gbp record): the file
+    is counted in 1 GiB pieces with a (k-1)-position overlap (main.fasta_pieces)
+    and the pieces' sorted results merged on the device.  The records repeat two
+    random 3 Mbp segments, so the expected counts follow from the oracle on short
+    strings: record 1 = (AB)^m -> m cnt(AB) + (m-1) J(BA), J(BA) = cnt(ABA) -
+    cnt(AB) - cnt(A); record 2 = A^n -> n cnt(A) + (n-1) (cnt(AA) - 2 cnt(A)).
+    The .npy must equal main.py:147-176 applied to those counts, bit for bit,
+    and the counts sum to the analytic window total.  The reference's Jellyfish
+    takes any file size (kf2vec/main.py:133-145)."""
+    import os
+    import shutil
+    from kf2vecfsw_amd import main as M
+    k, W = 21, 80
+    rng = np.random.default_rng(5150)
+    A, B = gen.random_seq(rng, 3_000_000), gen.random_seq(rng, 3_000_000)
+    m1, m2 = 780, 100
+    base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else str(tmp_path)
+    work = os.path.join(base, f"kf_5gib_{os.getpid()}")
+    os.makedirs(os.path.join(work, "in"))
+    try:
+        path = os.path.join(work, "in", "big.fna")
+        ab, a = gen.wrap(np.concatenate([A, B]), W), gen.wrap(A, W)   # 6 Mbp and 3 Mbp: whole lines
+        with open(path, "wb") as f:
+            f.write(b">r1 (AB)^780\n")
+            for _ in range(m1):
+                f.write(ab)
+            f.write(b">r2 A^100\n")
+            for _ in range(m2):
+                f.write(a)
+        size = os.path.getsize(path)
+        assert size > 5 * 10 ** 9 and size > (1 << 32)
+        M.main(["get_kmers", "-input_dir", os.path.join(work, "in"), "-output_dir", os.path.join(work, "out"),
+                "-k", str(k)])
+        got = np.load(os.path.join(work, "out", f"big_k{k}.npy"))
+        s = lambda x: oracle.sparse_count(b">x\n" + x.tobytes(), k)
+        cA, cAB, cABA, cAA = s(A), s(np.concatenate([A, B])), s(np.concatenate([A, B, A])), s(np.concatenate([A, A]))
+        ek, ec = _combine([(m1, *cAB), (m1 - 1, *cABA), (-(m1 - 1), *cAB), (-(m1 - 1), *cA),
+                           (m2, *cA), (m2 - 1, *cAA), (-2 * (m2 - 1), *cA)])
+        assert int(ec.sum()) == (m1 * 6_000_000 - k + 1) + (m2 * 3_000_000 - k + 1)
+        exp = M.sparse_kmers_matrix(ek.astype(np.uint64), ec, k)
+        assert got.shape == exp.shape and np.array_equal(got, exp)
+    finally:
+        shutil.rmtree(work, ignore_errors=True)

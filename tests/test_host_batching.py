@@ -4,6 +4,7 @@ time, kf2vec/main.py:301-357) and the up-front refusal of single files the
 32-bit per-call offsets cannot hold."""
 import os
 
+import numpy as np
 import pytest
 
 from kf2vecfsw_amd import main as M
@@ -74,3 +75,47 @@ def test_cli_host_threads_split_under_quota(monkeypatch, world, expect):
         assert M.cli_host_threads(args) == expect
     # -p below the quota is honoured, and a process never gets 0 threads
     assert M.host_threads(4, 1) == 4 and M.host_threads(4, 8) == 1 and M.host_threads(1, 16) == 1
+
+
+@pytest.mark.parametrize("k", [3, 9, 13, 21, 31])
+def test_fasta_pieces_count_every_window_once(tmp_path, oracle, k):
+    """get_kmers' pieces of a large FASTA file (main.fasta_pieces, here with tiny
+    pieces): counting every piece's bytes on its own and summing gives exactly
+    the whole file's canonical k-mer counts (no window lost or counted twice),
+    across line breaks, N runs, headers at and near the cuts, blank lines and
+    stray '>' bytes inside sequence lines.  Oracle = the restatement of
+    Jellyfish's counting (kf2vec/main.py:133-160)."""
+    import gen
+    rng = np.random.default_rng(k)
+    for t in range(6):
+        blob = gen.random_fasta(rng, int(rng.integers(2000, 20000)), max_records=int(rng.integers(1, 12)),
+                                n_rate=0.01, lower=0.05, poly_rate=0.01)
+        if t % 2:
+            arr = np.frombuffer(blob, np.uint8).copy()
+            pos = rng.integers(0, arr.size, 5)
+            arr[pos[arr[pos] != 10]] = ord(">")          # stray '>' bytes (resets, or new headers at line starts)
+            blob = arr.tobytes()
+        if t == 4:
+            blob = blob.replace(b"\n", b"\n\n\n")        # blank lines
+        p = tmp_path / f"g{t}.fna"
+        p.write_bytes(blob)
+        for piece in (64, 97, 1000):
+            parts = M.fasta_pieces(str(p), k, piece=piece)
+            assert parts[0][0] == 0 and parts[-1][1] == len(blob) and len(parts) >= len(blob) // piece // 2
+            assert all(a < e for a, e in parts)
+            if k <= 11:
+                whole, tot = oracle.count(blob, k)
+                got, gt = np.zeros_like(whole), 0
+                for a, e in parts:
+                    c, t_ = oracle.count(blob[a:e], k)
+                    got += c
+                    gt += t_
+                assert gt == tot and np.array_equal(got, whole), (t, piece)
+            else:
+                ek, ec = oracle.sparse_count(blob, k)
+                acc = {}
+                for a, e in parts:
+                    kk, cc = oracle.sparse_count(blob[a:e], k)
+                    for x, y in zip(kk.tolist(), cc.tolist()):
+                        acc[x] = acc.get(x, 0) + y
+                assert sorted(acc) == ek.tolist() and [acc[x] for x in ek.tolist()] == ec.tolist(), (t, piece)
