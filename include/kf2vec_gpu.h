@@ -126,22 +126,24 @@ int kf_index_fasta(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_gen
  *                flags & KF_ACCUMULATE
  *   d_totals   : n_genomes uint64, number of k-mers counted per genome
  * Asynchronous on `stream`.  For k >= 9 the library counts through a device
- * workspace (about 9 GB on a 256-CU device: 2 bytes of sorted records per byte
- * of the 8 MiB genome piece each CU holds, in two slots for the staggered
- * phases) plus a piece table of n_genomes+1 words, kept until
- * kf_workspace_release().  Both are allocated on first use; the piece table is
- * re-allocated behind a hipDeviceSynchronize() when n_genomes exceeds its
- * capacity (it grows at least 2x).  Call kf_workspace_reserve() first to keep
- * every kf_count_batch asynchronous and allocation-free.  Launches on different
- * streams of one device that use the workspace are ordered by the library. */
+ * workspace shared by every k >= 9 (about 10.7 GB on a 256-CU device: k = 9
+ * stages 2-byte records of up to 20 MiB of input per CU; k >= 10 keeps 2 bytes of
+ * sorted records per byte of the 8 MiB genome piece each CU holds, in two slots
+ * for the staggered phases) plus, for k >= 10, a piece table of n_genomes+1
+ * words, kept until kf_workspace_release().  Both are allocated on first use;
+ * the piece table is re-allocated behind a hipDeviceSynchronize() when
+ * n_genomes exceeds its capacity (it grows at least 2x).  Call
+ * kf_workspace_reserve() first to keep every kf_count_batch asynchronous and
+ * allocation-free.  Launches on different streams of one device that use the
+ * workspace are ordered by the library. */
 int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
                    const uint64_t* d_excl, uint64_t n_excl,
                    const uint32_t* d_code2col, const uint32_t* d_col2rep, int k,
                    uint32_t* d_counts, uint64_t* d_totals, uint32_t flags, void* stream);
 
 /* Allocate up front, on the current device, everything kf_count_batch(k, n)
- * needs for any n <= max_genomes: the k >= 9 bucket tables, workspace and piece
- * table, and the kernel attributes of k.  Afterwards such calls neither
+ * needs for any n <= max_genomes: the k >= 9 workspace, the k >= 10 bucket
+ * tables and piece table, and the kernel attributes of k.  Afterwards such calls neither
  * allocate nor synchronise.  Synchronous; may be called again with a larger
  * max_genomes. */
 int kf_workspace_reserve(int k, int32_t max_genomes);
@@ -150,8 +152,10 @@ int kf_workspace_reserve(int k, int32_t max_genomes);
  * threads per workgroup, dynamic LDS bytes); for roofline accounting.
  * Kernel choice: k <= 7 the pair kernel K1x (k1x_kernel<k>: (k+1)-mer pairs
  * plus single k-mers in LDS), k = 8 its single-pass form (k1x_kernel<8>),
- * k >= 9 the two-phase bucket kernels (bucket_kernel<k>).  No environment
- * variable changes the choice. */
+ * k = 9 the one-pass staged kernel (k9s_kernel: half the canonical classes in
+ * LDS, the other half staged to HBM as 2-byte records and counted after the
+ * first half's flush), k >= 10 the two-phase bucket kernels (bucket_kernel<k>).
+ * No environment variable changes the choice in the product library. */
 int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
 
 /* ---- get_kmers at any k = 2..31 (replaces `jellyfish count -m K -C` +
