@@ -532,12 +532,22 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
     uint32_t* gcounts = A.counts + (uint64_t)g * A.nbins;
     Range rg;
     rg.init(glo, ghi, lo, hi);
-    XBlock buf[kXRing];
     auto load = [&](uint32_t r) {
         return xc_load(A.bytes, rg.c0, r, rg.end_r, lane);
     };
+    // k <= 8: the ring as an array the compiler unrolls into registers; k = 9's
+    // step is too large for that unroll, so its ring is two named blocks (an
+    // array it cannot unroll would be indexed in scratch memory)
+    static_assert(kXRing == 2, "two-deep register ring");
+    XBlock buf[K == 9 ? 1 : kXRing];
+    XBlock b0, b1;
+    if constexpr (K == 9) {
+        b0 = load(0);
+        b1 = load(kXChunk);
+    } else {
 #pragma unroll
-    for (int j = 0; j < kXRing; ++j) buf[j] = load(j * kXChunk);
+        for (int j = 0; j < kXRing; ++j) buf[j] = load(j * kXChunk);
+    }
     const uint32_t nx = (rg.nch + 2) / 3;   // 3 KiB iterations
     rg.warm16<K>(A, lane);
     __builtin_amdgcn_s_setprio(0);   // (the setup ran at top priority, see k1x_kernel)
@@ -578,17 +588,27 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
         }
         rel += kXChunk;
     };
-    for (uint32_t i = 0; i + kXRing <= nx; i += kXRing) {
-#pragma unroll
-        for (int j = 0; j < kXRing; ++j) {
-            step(buf[j]);
-            buf[j] = load(rel + (kXRing - 1) * kXChunk);
+    if constexpr (K == 9) {
+        for (uint32_t i = 0; i + 2 <= nx; i += 2) {
+            step(b0);
+            b0 = load(rel + kXChunk);
+            step(b1);
+            b1 = load(rel + kXChunk);
         }
-    }
-    const uint32_t rem = nx % kXRing;
+        if (nx & 1u) step(b0);
+    } else {
+        for (uint32_t i = 0; i + kXRing <= nx; i += kXRing) {
 #pragma unroll
-    for (int j = 0; j < kXRing - 1; ++j)
-        if (rem > (uint32_t)j) step(buf[j]);
+            for (int j = 0; j < kXRing; ++j) {
+                step(buf[j]);
+                buf[j] = load(rel + (kXRing - 1) * kXChunk);
+            }
+        }
+        const uint32_t rem = nx % kXRing;
+#pragma unroll
+        for (int j = 0; j < kXRing - 1; ++j)
+            if (rem > (uint32_t)j) step(buf[j]);
+    }
     return lane_total + 48u * nfast;
 }
 
