@@ -386,27 +386,39 @@ __device__ __forceinline__ K9Win k9_window(const XcCls& k, uint32_t rot) {
 // wave's record stream.  A region holds at most 1,024 part-1 windows: the
 // staging area.  The LDS reads of the copy-out precede the next region's writes
 // in the wave's LDS order.
+template <bool DENSE>
 __device__ __forceinline__ uint32_t k9_region(uint32_t wlo, uint32_t whi, uint32_t R, int lane, K9Out& so) {
+    // DENSE (fast path): windows 0..14 are counted, window 15 unless R says
+    // otherwise (a newline in the region); else R gives every window.
     const uint32_t rlo = revpairs(whi) ^ 0xAAAAAAAAu, rhi = revpairs(wlo) ^ 0xAAAAAAAAu;
-    uint32_t o = 0, n1 = 0;
+    uint32_t n1 = 0;
     const uint32_t sb = so.stage >> 1;   // staging slot base (u16 units)
+    // the adds' returns go to registers zeroed first and are ORed after the
+    // last window: an add under a lane test whose return were used inside the
+    // test would wait for it there (one LDS round trip per window)
+    uint32_t rt[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rt[r] = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const uint32_t y = __builtin_amdgcn_alignbit(whi, wlo, 2 * r);            // bits above 17: other windows
+        const uint32_t y = r < 8 ? wlo >> (2 * r) : __builtin_amdgcn_alignbit(whi, wlo, 2 * r);   // bits above 17: junk
         const uint32_t rc = r < 8 ? rhi >> (14 - 2 * r) : __builtin_amdgcn_alignbit(rhi, rlo, 46 - 2 * r);
         const uint32_t c = bfi((uint32_t)__builtin_amdgcn_sbfe((int)y, 9u, 1u), rc, y);   // class (18 low bits)
         const uint32_t ki = bfi(0x1FFu, c, c >> 1);                                     // index; part at bit 16
-        const bool v = (R >> r) & 1u;
-        const bool p1 = (c >> 17) & 1u;
-        if (v && !p1) o |= lds_add_rtn((ki << 1) & 0x1FFFCu, 1u << ((ki << 4) & 31u));
-        const uint64_t m = __builtin_amdgcn_ballot_w64(v && p1);
-        if (v && p1) {
+        const uint32_t vb = (DENSE && r < 15) ? 1u : ((R >> r) & 1u);                  // window counted
+        const uint32_t s1 = (ki >> 16) & vb;                                            // staged (part 1)
+        if (vb > s1) rt[r] = lds_add_rtn((ki << 1) & 0x1FFFCu, 1u << ((ki << 4) & 31u));
+        const uint64_t m = __builtin_amdgcn_ballot_w64(s1 != 0);
+        if (s1) {
             const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, sb + n1));
             *(lds_u16*)(uintptr_t)(2u * slot) = (uint16_t)ki;
         }
         n1 += (uint32_t)__builtin_popcountll(m);
     }
+    uint32_t o = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o |= rt[r];
     const uint32_t pads = (0u - n1) & 7u;
     if ((uint32_t)lane < pads) *(lds_u16*)(uintptr_t)(so.stage + 2u * (n1 + (uint32_t)lane)) = (uint16_t)0xFFFFu;
     const uint32_t units = (n1 + 7u) >> 3;
@@ -439,11 +451,11 @@ __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int
         // each region's window register, then its 16 windows (window 15 of a
         // region with a newline belongs to lane L-1's region: not counted)
         const K9Win x0 = k9_window(k0, t_codes(carry));
-        uint32_t o = k9_region(x0.wlo, x0.whi, 0xFFFFu >> x0.nl, lane, *so);
+        uint32_t o = k9_region<true>(x0.wlo, x0.whi, 0xFFFFu >> x0.nl, lane, *so);
         const K9Win x1 = k9_window(k1, wave_ror1(x0.c));
-        o |= k9_region(x1.wlo, x1.whi, 0xFFFFu >> x1.nl, lane, *so);
+        o |= k9_region<true>(x1.wlo, x1.whi, 0xFFFFu >> x1.nl, lane, *so);
         const K9Win x2 = k9_window(k2, wave_ror1(x1.c));
-        o |= k9_region(x2.wlo, x2.whi, 0xFFFFu >> x2.nl, lane, *so);
+        o |= k9_region<true>(x2.wlo, x2.whi, 0xFFFFu >> x2.nl, lane, *so);
         lane_total -= x0.nl + x1.nl + x2.nl;
         carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)x2.c, kWave - 1) & TM, 31u, 31u);
         if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
@@ -497,7 +509,7 @@ __device__ __forceinline__ uint32_t x_singles(const uint4 d, const CountArgs& A,
     const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
     const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
     if constexpr (K == 9) {   // every counted window through the k = 9 region step
-        const uint32_t o9 = k9_region(wlo, whi, R, lane, *so);
+        const uint32_t o9 = k9_region<false>(wlo, whi, R, lane, *so);
         if (__builtin_amdgcn_ballot_w64((o9 & HOT) != 0) != 0) {
             x_scan_drain<K>(A.code2col, gcounts, lane);
             drained = 1;
