@@ -104,20 +104,22 @@ def _object(src: str, cmd_tail: list[str], csrc: str = CSRC) -> tuple[str, bool]
     return o, os.path.exists(o)
 
 
-ABL_PATCH = os.path.join(HERE, "..", "tools", "zoo", "bucket_ablations.patch")
+ABL_PATCHES = [os.path.join(HERE, "..", "tools", "zoo", f) for f in ("bucket_ablations.patch", "k9s_ablations.patch")]
 
 
 def _ablation_sources() -> str:
-    """A copy of csrc/ (and the header) with tools/zoo/bucket_ablations.patch
-    applied: the bucket kernels' KF_BK_ABL=n profiling ablations (wrong counts by
-    design), kept out of the product source.  Returns its csrc directory."""
+    """A copy of csrc/ (and the header) with tools/zoo/*_ablations.patch applied:
+    the bucket kernels' KF_BK_ABL=n and K9s's KF_K9_ABL=n profiling ablations
+    (wrong counts by design), kept out of the product source.  Returns its csrc
+    directory."""
     import shutil
     root = os.path.join(BUILD, "abl_src")
     shutil.rmtree(root, ignore_errors=True)
     shutil.copytree(CSRC, os.path.join(root, "kf2vecfsw_amd", "csrc"))
     os.makedirs(os.path.join(root, "include"))
     shutil.copy(os.path.join(HERE, "..", "include", "kf2vec_gpu.h"), os.path.join(root, "include"))
-    subprocess.run(["patch", "-s", "-p1", "-d", root, "-i", os.path.abspath(ABL_PATCH)], check=True)
+    for p in ABL_PATCHES:
+        subprocess.run(["patch", "-s", "-p1", "-d", root, "-i", os.path.abspath(p)], check=True)
     return os.path.join(root, "kf2vecfsw_amd", "csrc")
 
 
