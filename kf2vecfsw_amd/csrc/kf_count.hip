@@ -431,6 +431,78 @@ __device__ __forceinline__ uint32_t k9_region(uint32_t wlo, uint32_t whi, uint32
     return o;
 }
 
+// ---------------------------------------------------------------- K9b (k = 9, the product)
+// All 131,072 classes as u8 counters in LDS (class index i at byte i: word
+// i >> 2, byte i & 3; 128 KiB), one pass, no staging.  A byte wraps every 256
+// adds; the carry then runs into the bytes above it in the word.  Every add
+// returns the word's old value and is atomic, so the lane whose add carries
+// sees it exactly: a byte b at 0xFF before the add means class b wrapped (+256
+// to its row column) and byte b+1 got a carry that is no count of its class
+// (-1), which wraps in turn if it was at 0xFF (+256, carry on), up to byte 3
+// (the carry out of the word is lost).  Those corrections go to the count row
+// by global atomics (once per 256 adds of a class at most), the LDS bytes keep
+// the counts mod 256, and the flush adds them.  Per window: the class, one LDS
+// add, and a two-op check of its return (the byte's old value is 0xFF) folded
+// into one max per region; only a region with a wrap walks its windows again.
+// Class index (17 bits) of window r of the window register (wlo, whi), whose
+// reverse complement is (rlo, rhi).
+__device__ __forceinline__ uint32_t k9_index(uint32_t wlo, uint32_t whi, uint32_t rlo, uint32_t rhi, int r) {
+    const uint32_t y = r < 8 ? wlo >> (2 * r) : __builtin_amdgcn_alignbit(whi, wlo, 2 * r);
+    const uint32_t rc = r < 8 ? rhi >> (14 - 2 * r) : __builtin_amdgcn_alignbit(rhi, rlo, 46 - 2 * r);
+    const uint32_t c = bfi((uint32_t)__builtin_amdgcn_sbfe((int)y, 9u, 1u), rc, y);
+    return bfi(0x1FFu, c, c >> 1) & 0x1FFFFu;
+}
+
+// The exact carry corrections of one region (rare: out of line, so its
+// registers do not weigh on the counting loop).  Returns 1 if any lane made one.
+__device__ __noinline__ uint32_t k9b_carries(uint32_t wlo, uint32_t whi, const uint32_t* __restrict__ code2col,
+                                             uint32_t* gcounts, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                             uint32_t w4, uint32_t w5, uint32_t w6, uint32_t w7, uint32_t w8,
+                                             uint32_t w9, uint32_t w10, uint32_t w11, uint32_t w12, uint32_t w13,
+                                             uint32_t w14, uint32_t w15) {
+    const uint32_t rlo = revpairs(whi) ^ 0xAAAAAAAAu, rhi = revpairs(wlo) ^ 0xAAAAAAAAu;
+    const uint32_t rt[16] = {w0, w1, w2, w3, w4, w5, w6, w7, w8, w9, w10, w11, w12, w13, w14, w15};
+    uint32_t fixed = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t w = rt[r], ki = k9_index(wlo, whi, rlo, rhi, r), b = ki & 3u;
+        if (((w >> (8 * b)) & 0xFFu) != 0xFFu) continue;   // (a window not counted has w = 0)
+        const uint32_t base = ki & ~3u;
+        fixed = 1;
+        atomicAdd(gcounts + code2col[k9_code_of(base | b)], 256u);
+        for (uint32_t j = b + 1; j < 4; ++j) {   // the carry into byte j
+            const uint32_t col = code2col[k9_code_of(base | j)];
+            const bool wraps = ((w >> (8 * j)) & 0xFFu) == 0xFFu;
+            atomicAdd(gcounts + col, wraps ? 255u : 0xFFFFFFFFu);   // -1, +256 if it wrapped too
+            if (!wraps) break;
+        }
+    }
+    return __builtin_amdgcn_ballot_w64(fixed != 0) != 0 ? 1u : 0u;
+}
+
+template <bool DENSE>
+__device__ __forceinline__ uint32_t k9b_region(uint32_t wlo, uint32_t whi, uint32_t R, const CountArgs& A,
+                                               uint32_t* gcounts) {
+    const uint32_t rlo = revpairs(whi) ^ 0xAAAAAAAAu, rhi = revpairs(wlo) ^ 0xAAAAAAAAu;
+    uint32_t rt[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t ki = k9_index(wlo, whi, rlo, rhi, r);
+        rt[r] = 0;   // (a window not counted: no byte of 0 is 0xFF)
+        const bool v = (DENSE && r < 15) || ((R >> r) & 1u);
+        if (v) rt[r] = lds_add_rtn(ki & 0x1FFFCu, 1u << ((ki << 3) & 24u));
+    }
+    // any byte of an old word at 0xFF (its add may have carried): ~(w + 0x01..)
+    // & w has bit 7 of byte j set iff byte j of w is 0xFF (a borrow-free test);
+    // another class's byte at 0xFF only sends the region down the exact path
+    uint32_t acc = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc |= ~(rt[r] + 0x01010101u) & rt[r];
+    if (__builtin_amdgcn_ballot_w64((acc & 0x80808080u) != 0) == 0) return 0;
+    return k9b_carries(wlo, whi, A.code2col, gcounts, rt[0], rt[1], rt[2], rt[3], rt[4], rt[5], rt[6], rt[7], rt[8],
+                       rt[9], rt[10], rt[11], rt[12], rt[13], rt[14], rt[15]);
+}
+
 // Fast case of a coalesced 3 KiB iteration (uniform): every region of every lane
 // is bases with at most one newline and the carry is complete; returns false
 // (nothing counted) otherwise.  u16 exactness: every add's return is checked at
@@ -438,7 +510,9 @@ __device__ __forceinline__ uint32_t k9_region(uint32_t wlo, uint32_t whi, uint32
 // at most one more iteration to it before its own drain.  k = 7: at most 24 x 64
 // adds per wave and iteration, so a half stays below 0x4000 + 16 x 1536 = 0xA000;
 // k = 8: 48 x 64, below 0x2000 + 16 x 3072 = 0xE000.
-template <int K>
+// M9 (k = 9 only): 1 = K9b (byte counters, the product), 2 = K9s (staged part 1
+// through *so; profiling builds)
+template <int K, int M9 = 1>
 __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
                                         uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained, K9Out* so) {
     constexpr uint32_t HOT = x_hot<K>();
@@ -450,6 +524,18 @@ __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int
     if constexpr (K == 9) {
         // each region's window register, then its 16 windows (window 15 of a
         // region with a newline belongs to lane L-1's region: not counted)
+        if constexpr (M9 == 1) {   // K9b: byte counters (no drains: carries are fixed as they happen)
+            const K9Win x0 = k9_window(k0, t_codes(carry));
+            uint32_t f = k9b_region<true>(x0.wlo, x0.whi, 0xFFFFu >> x0.nl, A, gcounts);
+            const K9Win x1 = k9_window(k1, wave_ror1(x0.c));
+            f |= k9b_region<true>(x1.wlo, x1.whi, 0xFFFFu >> x1.nl, A, gcounts);
+            const K9Win x2 = k9_window(k2, wave_ror1(x1.c));
+            f |= k9b_region<true>(x2.wlo, x2.whi, 0xFFFFu >> x2.nl, A, gcounts);
+            lane_total -= x0.nl + x1.nl + x2.nl;
+            carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)x2.c, kWave - 1) & TM, 31u, 31u);
+            drained |= f;
+            return true;
+        }
         const K9Win x0 = k9_window(k0, t_codes(carry));
         uint32_t o = k9_region<true>(x0.wlo, x0.whi, 0xFFFFu >> x0.nl, lane, *so);
         const K9Win x1 = k9_window(k1, wave_ror1(x0.c));
@@ -499,7 +585,7 @@ __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int
 // Irregular 1 KiB chunk (16-byte lane layout, the general front end): every
 // counted window as a single by its forward code -- into S (k = 7) or P
 // (k = 8) -- with its return checked at once.
-template <int K, bool MASKED>
+template <int K, bool MASKED, int M9 = 1>
 __device__ __forceinline__ uint32_t x_singles(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
                                               const ChunkMask& m, uint64_t iv0, uint32_t carry, uint32_t* gcounts,
                                               uint32_t& lane_total, uint32_t& drained, K9Out* so) {
@@ -509,6 +595,11 @@ __device__ __forceinline__ uint32_t x_singles(const uint4 d, const CountArgs& A,
     const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
     const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
     if constexpr (K == 9) {   // every counted window through the k = 9 region step
+        if constexpr (M9 == 1) {   // K9b
+            drained |= k9b_region<false>(wlo, whi, R, A, gcounts);
+            lane_total += (uint32_t)__builtin_popcount(R);
+            return win.next;
+        }
         const uint32_t o9 = k9_region<false>(wlo, whi, R, lane, *so);
         if (__builtin_amdgcn_ballot_w64((o9 & HOT) != 0) != 0) {
             x_scan_drain<K>(A.code2col, gcounts, lane);
@@ -537,7 +628,7 @@ __device__ __forceinline__ uint32_t x_singles(const uint4 d, const CountArgs& A,
 // The wave range [lo, hi) of genome [glo, ghi) in 3 KiB iterations (K1x).
 // `drained` is set if a u16 half of this range was moved to the count row (the
 // flush then adds with atomics).
-template <int K>
+template <int K, int M9 = 1>
 __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi, uint64_t lo,
                                             uint64_t hi, int lane, uint32_t& drained, K9Out* so = nullptr) {
     if (lo >= hi) return 0;
@@ -572,7 +663,7 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
         // one test for the whole 3 KiB (range edges, excluded intervals)
         bool fast = !rg.masked_span(A, rel, kXChunk);
         if (fast)
-            fast = xc_fast<K>(bf, A, lane, carry, gcounts, lane_total, drained, so);
+            fast = xc_fast<K, M9>(bf, A, lane, carry, gcounts, lane_total, drained, so);
         nfast += fast ? 1u : 0u;
         if (!fast) {
             // interval cursor before each 1 KiB third (a later test may advance it)
@@ -591,11 +682,11 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
                 // the coalesced block already holds this third in the 16-byte lane layout
                 const uint4 hb = bf.q[h];
                 if (mh)
-                    carry = x_singles<K, true>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained,
-                                               so);
+                    carry = x_singles<K, true, M9>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total,
+                                                   drained, so);
                 else
-                    carry = x_singles<K, false>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained,
-                                                so);
+                    carry = x_singles<K, false, M9>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total,
+                                                    drained, so);
             }
         }
         rel += kXChunk;
@@ -673,7 +764,7 @@ __device__ __forceinline__ void pair_f_sums_small(const uint32_t* hist, int tid,
 
 template <int K>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) k1x_kernel(CountArgs A) {
-    static_assert(K >= 2 && K <= 8, "K1x serves k = 2 .. 8");
+    static_assert(K >= 2 && K <= 9, "K1x serves k = 2 .. 9 (k = 9: K9b byte counters)");
     // P and S (the whole dynamic LDS, at address 0: see lds_add); no LDS is left
     // for reduction slots, so totals go straight to global atomics
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
@@ -708,7 +799,35 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 
         // other workgroup and nothing else touches row g, which the caller
         // zeroed, so it is written with plain stores; otherwise atomics.
         const bool whole = plo == glo && phi == ghi && !(A.flags & KF_ACCUMULATE);
-        if constexpr (K == 8) {
+        if constexpr (K == 9) {
+            // every column in order (coalesced row writes): its class's byte;
+            // rows with carry corrections (already added to them) take atomics
+            lds_barrier();   // every add of this piece is done
+            if (lane == 0) hist[XL<K>::P / 4 + wave] = drained;
+            lds_barrier();
+            const uint4* fl = (const uint4*)(hist + XL<K>::P / 4);
+            const uint4 f0 = fl[0], f1 = fl[1], f2 = fl[2], f3 = fl[3];
+            const bool any_fix = (f0.x | f0.y | f0.z | f0.w | f1.x | f1.y | f1.z | f1.w | f2.x | f2.y | f2.z |
+                                  f2.w | f3.x | f3.y | f3.z | f3.w) != 0;
+            const uint8_t* hb = (const uint8_t*)hist;
+            for (uint32_t c0 = (uint32_t)tid; c0 < (1u << 17); c0 += 4 * kBlock) {
+                uint32_t rep[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) rep[j] = A.col2rep[c0 + j * kBlock];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t c = (rep[j] & 0x200u) ? kf_revcomp<9>(rep[j]) : rep[j];
+                    const uint32_t v = hb[((c >> 1) & 0x1FE00u) | (c & 0x1FFu)];
+                    if (whole && !any_fix)
+                        __builtin_nontemporal_store(v, gc + c0 + j * kBlock);
+                    else if (v)
+                        __hip_atomic_fetch_add(gc + c0 + j * kBlock, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            lds_barrier();   // bytes read
+            uint4* h4 = (uint4*)hist;
+            for (uint32_t i = tid; i < XL<K>::bytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+        } else if constexpr (K == 8) {
             // canonical 8-mer column = P[rep] + P[rc rep] (a palindrome once);
             // drain flags in the (unused) S area
             lds_barrier();   // every add of this piece is done
@@ -993,7 +1112,7 @@ k9s_kernel(CountArgs A, uint16_t* scratch, uint64_t wg_records) {
             so.pads = 0;
             so.stage = XL<9>::P + (uint32_t)wave * kK9Stage;
             uint32_t drained0 = 0;
-            unsigned long long s = x_range<9>(A, g, glo, ghi, lo, hi, lane, drained0, &so);
+            unsigned long long s = x_range<9, 2>(A, g, glo, ghi, lo, hi, lane, drained0, &so);
             __builtin_amdgcn_s_setprio(0);
             uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
             uint32_t* gcounts = gc;
@@ -1169,7 +1288,7 @@ void* kernel_for(int k) {
     case 6: return (void*)&k1x_kernel<6>;
     case 7: return (void*)&k1x_kernel<7>;
     case 8: return (void*)&k1x_kernel<8>;
-    case 9: return (void*)&k9s_kernel;
+    case 9: return (void*)&k1x_kernel<9>;
     default: return nullptr;
     }
 }
@@ -1191,7 +1310,7 @@ int lds_bytes_for(int k) {
 // k = 9: records scratch per workgroup (one segment's bytes, 2 B each, plus the
 // wave ranges' 16-byte alignment) and its total for `grid` workgroups
 constexpr uint64_t kK9WgRecords = kK9SegMax + 1024;
-uint64_t k9_scratch_bytes(int grid) { return (uint64_t)grid * kK9WgRecords * 2; }
+[[maybe_unused]] uint64_t k9_scratch_bytes(int grid) { return (uint64_t)grid * kK9WgRecords * 2; }
 
 // grid per (k, device): workgroups per CU from the occupancy API x CUs
 int g_grid[KF_MAX_K + 1][64];
@@ -1234,9 +1353,7 @@ extern "C" int kf_workspace_reserve(int k, int32_t max_genomes) {
     if (max_genomes < 0) return kf_fail(KF_EINVAL, "max_genomes < 0");
     if (k >= 10) return bucket_reserve(k, max_genomes);
     int grid = 0, block = 0, lds = 0;   // the kernel attribute and grid of k
-    const int rc = launch_info(k, &grid, &block, &lds);
-    if (rc || k != 9) return rc;
-    return scratch_reserve(k9_scratch_bytes(grid));   // k = 9: the records scratch
+    return launch_info(k, &grid, &block, &lds);
 }
 
 extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_genomes,
@@ -1281,7 +1398,13 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     int grid = 0, block = 0, lds = 0;
     const int rc = launch_info(k, &grid, &block, &lds);
     if (rc) return rc;
-    if (k == 9) {   // K9s: the records scratch is the library's shared device scratch
+#ifdef KF_PROFILE_BUILD
+    // profiling builds: KF_K9_STAGED=1 counts k = 9 with K9s (half the classes
+    // staged to HBM; round 6's first k = 9 kernel), for A/B against K9b
+    if (k == 9 && getenv("KF_K9_STAGED") && atoi(getenv("KF_K9_STAGED"))) {
+        if (hipFuncSetAttribute((const void*)&k9s_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+            hipSuccess)
+            return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
         return scratch_launch(k9_scratch_bytes(grid), s, [&](void* scratch) {
             uint16_t* rec = (uint16_t*)scratch;
             uint64_t wg = kK9WgRecords;
@@ -1291,6 +1414,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
             return (int)KF_OK;
         });
     }
+#endif
     void* args[] = {&A};
     if (hipLaunchKernel(kernel_for(k), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));

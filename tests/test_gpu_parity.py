@@ -540,6 +540,24 @@ def test_k9_staged_part1_heavy_and_periodic(torch_dev, oracle):
     check_against_oracle(oracle, blobs, 9, counts, totals, tag="k9s")
 
 
+def test_k9_byte_counter_carry_chains(torch_dev, oracle):
+    """K9b (k = 9 in u8 LDS counters, 4 classes per word): the classes AAAAAAAAx
+    (x = A, C, T, G) share one word, and sequence built from long A runs broken
+    by single C, G and T keeps all four bytes cycling through 0xFF, so adds wrap
+    their byte, carry into the next one, and carries arrive at bytes already at
+    0xFF (chains); every correction must land exactly.  Also GGGGAGGGG-style
+    classes of part 1 and a genome whose rows get no correction at all."""
+    rng = np.random.default_rng(4711)
+    units = [b"A" * int(rng.integers(9, 40)) + bytes([rng.choice([67, 71, 84])]) for _ in range(2000)]
+    blob = b"".join(units[i % len(units)] for i in range(120_000))
+    blobs = [b">chains\n" + gen.wrap(np.frombuffer(blob, np.uint8), 80),
+             b">mix\n" + gen.wrap(np.frombuffer((b"AAAAAAAAAC" * 3 + b"AAAAAAAAAG" * 2 + b"TTTTTTTTT") * 90_000,
+                                                 np.uint8), 61),
+             b">few\n" + gen.wrap(gen.random_seq(rng, 30_000), 80)]
+    counts, totals = run_batch(blobs, 9, torch_dev)
+    check_against_oracle(oracle, blobs, 9, counts, totals, tag="k9b")
+
+
 def test_k9_two_segments_every_genome(torch_dev, oracle):
     """K9s splits a batch into G x ceil(total / (G x 20 MiB)) segments: 1,200 x 5
     Mbp (6.07 GB, N runs) gives every workgroup two, so its record scratch is
