@@ -414,8 +414,7 @@ def by_k_bench(W, dbs, args, workload_tag: str) -> dict:
                                     "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                                     "frac": round(alg / (km * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
                                     "traffic": tr, "traffic_source": src},
-                       "kernel": ("k1x_kernel<%d>" % k) if k <= 8 else "k9s_kernel" if k == 9
-                       else ("bucket_kernel<%d>" % k),
+                       "kernel": ("k1x_kernel<%d>" % k) if k <= 9 else ("bucket_kernel<%d>" % k),
                        "launch": [grid, block, lds], "parity": "ok" if okk else "MISMATCH"}
         del kc, o
         torch.cuda.empty_cache()

@@ -16,7 +16,7 @@
  *     e.g. `torch.Tensor.data_ptr()` of a ROCm tensor; the CALLER owns every buffer;
  *   - `stream` is a hipStream_t (NULL = default stream); device entry points only
  *     enqueue work, so they can be graph-captured -- with one exception:
- *     kf_count_batch at k >= 9 allocates the library's workspace on first use
+ *     kf_count_batch at k >= 10 allocates the library's workspace on first use
  *     and grows its piece table (a device sync) when n_genomes exceeds every
  *     earlier call; kf_workspace_reserve() does both up front;
  *   - return 0 on success, a negative KF_E* code on failure; the message is in
@@ -125,12 +125,11 @@ int kf_index_fasta(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_gen
  *   d_counts   : n_genomes x nbins uint32 (column order), zeroed first unless
  *                flags & KF_ACCUMULATE
  *   d_totals   : n_genomes uint64, number of k-mers counted per genome
- * Asynchronous on `stream`.  For k >= 9 the library counts through a device
- * workspace shared by every k >= 9 (about 10.7 GB on a 256-CU device: k = 9
- * stages 2-byte records of up to 20 MiB of input per CU; k >= 10 keeps 2 bytes of
- * sorted records per byte of the 8 MiB genome piece each CU holds, in two slots
- * for the staggered phases) plus, for k >= 10, a piece table of n_genomes+1
- * words, kept until kf_workspace_release().  Both are allocated on first use;
+ * Asynchronous on `stream`.  For k >= 10 the library counts through a device
+ * workspace (about 9 GB on a 256-CU device: 2 bytes of sorted records per byte
+ * of the 8 MiB genome piece each CU holds, in two slots for the staggered
+ * phases) plus a piece table of n_genomes+1 words, kept until
+ * kf_workspace_release().  Both are allocated on first use;
  * the piece table is re-allocated behind a hipDeviceSynchronize() when
  * n_genomes exceeds its capacity (it grows at least 2x).  Call
  * kf_workspace_reserve() first to keep every kf_count_batch asynchronous and
@@ -142,8 +141,8 @@ int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n_gen
                    uint32_t* d_counts, uint64_t* d_totals, uint32_t flags, void* stream);
 
 /* Allocate up front, on the current device, everything kf_count_batch(k, n)
- * needs for any n <= max_genomes: the k >= 9 workspace, the k >= 10 bucket
- * tables and piece table, and the kernel attributes of k.  Afterwards such calls neither
+ * needs for any n <= max_genomes: the k >= 10 bucket tables, workspace and
+ * piece table, and the kernel attributes of k.  Afterwards such calls neither
  * allocate nor synchronise.  Synchronous; may be called again with a larger
  * max_genomes. */
 int kf_workspace_reserve(int k, int32_t max_genomes);
@@ -152,9 +151,9 @@ int kf_workspace_reserve(int k, int32_t max_genomes);
  * threads per workgroup, dynamic LDS bytes); for roofline accounting.
  * Kernel choice: k <= 7 the pair kernel K1x (k1x_kernel<k>: (k+1)-mer pairs
  * plus single k-mers in LDS), k = 8 its single-pass form (k1x_kernel<8>),
- * k = 9 the one-pass staged kernel (k9s_kernel: half the canonical classes in
- * LDS, the other half staged to HBM as 2-byte records and counted after the
- * first half's flush), k >= 10 the two-phase bucket kernels (bucket_kernel<k>).
+ * k = 9 its byte-counter form (k1x_kernel<9>: all 131,072 canonical classes
+ * as u8 LDS counters, carries corrected exactly from the adds' returns), k >= 10
+ * the two-phase bucket kernels (bucket_kernel<k>).
  * No environment variable changes the choice in the product library. */
 int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
 

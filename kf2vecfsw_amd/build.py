@@ -104,14 +104,13 @@ def _object(src: str, cmd_tail: list[str], csrc: str = CSRC) -> tuple[str, bool]
     return o, os.path.exists(o)
 
 
-ABL_PATCHES = [os.path.join(HERE, "..", "tools", "zoo", f) for f in ("bucket_ablations.patch", "k9s_ablations.patch")]
+ABL_PATCHES = [os.path.join(HERE, "..", "tools", "zoo", "bucket_ablations.patch")]
 
 
 def _ablation_sources() -> str:
-    """A copy of csrc/ (and the header) with tools/zoo/*_ablations.patch applied:
-    the bucket kernels' KF_BK_ABL=n and K9s's KF_K9_ABL=n profiling ablations
-    (wrong counts by design), kept out of the product source.  Returns its csrc
-    directory."""
+    """A copy of csrc/ (and the header) with tools/zoo/bucket_ablations.patch
+    applied: the bucket kernels' KF_BK_ABL=n profiling ablations (wrong counts by
+    design), kept out of the product source.  Returns its csrc directory."""
     import shutil
     root = os.path.join(BUILD, "abl_src")
     shutil.rmtree(root, ignore_errors=True)

@@ -1164,30 +1164,6 @@ int ensure_scratch(DevState& d, int dev, size_t need) {
     return KF_OK;
 }
 
-int scratch_reserve(size_t bytes) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
-    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
-    std::lock_guard<std::mutex> lk(g_mu);
-    return ensure_scratch(g_dev[dev], dev, bytes);
-}
-
-int scratch_launch(size_t bytes, hipStream_t s, const std::function<int(void*)>& launch) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");
-    if (dev < 0 || dev >= 64) return kf_fail(KF_EINVAL, "device index out of range");
-    std::lock_guard<std::mutex> lk(g_mu);
-    DevState& d = g_dev[dev];
-    int rc = ensure_scratch(d, dev, bytes);
-    if (rc) return rc;
-    if (d.done && hipStreamWaitEvent(s, d.done, 0) != hipSuccess)
-        return kf_fail(KF_EHIP, "hipStreamWaitEvent failed");
-    rc = launch(d.scratch);
-    if (rc) return rc;
-    if (hipEventRecord(d.done, s) != hipSuccess) return kf_fail(KF_EHIP, "hipEventRecord failed");
-    return KF_OK;
-}
-
 int bucket_reserve(int k, int32_t max_genomes) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return kf_fail(KF_EHIP, "hipGetDevice failed");

@@ -30,10 +30,9 @@
 //       to the count row (exact: see xc_fast);
 //   K1x8 k1x_kernel<8> (k = 8): the K1x front end with every window an 8-mer
 //       in P (one pass over the bytes).
-//   K9s  k9s_kernel (k = 9, round 6): the K1x front end; every window's
-//       canonical class is computed once; half the classes (part 0) are counted
-//       in P, the other half staged through LDS to HBM as 16-bit records and
-//       counted in P after part 0's flush (see "K9s" below).
+//   K9b  k1x_kernel<9> (k = 9, round 6): the K1x front end, every window's
+//       canonical class once, all 131,072 classes as u8 counters in LDS whose
+//       byte carries are corrected exactly from the adds' returns (see "K9b").
 // (Rounds 1-3 counted k <= 6 with one u32 LDS add per window, K1.)
 // Rejected alternatives and their measurements live in tools/zoo/ (DESIGN.md).
 #include <hip/hip_runtime.h>
@@ -99,25 +98,13 @@ constexpr uint32_t x_hot() { return K >= 8 ? kHot8 : (K == 7 ? kHot7 : kHot6); }
 template <int K>
 constexpr uint32_t x_step() { return K >= 8 ? kStep8 : (K == 7 ? kStep7 : kStep6); }
 
-// ---------------------------------------------------------------- K9s geometry
-// k = 9 has 131,072 canonical classes (4^9 / 2: k odd, no palindromes), two
-// 65,536-entry parts.  Class of a 9-mer y (kf code, first base highest): its
-// orientation whose middle base is A or C, i.e. kf-code bit 9 clear -- the
-// reverse complement flips that bit -- so c = bit9(y) ? rc(y) : y.  Its index is
-// c without bit 9, i = (c & 0x1FF) | (c >> 1 & 0x1FE00) (17 bits); part =
-// i >> 16 (first base T or G).  Part-local index i & 0xFFFF = u16 half (i & 1)
-// of P word (i & 0xFFFF) >> 1.
-constexpr uint32_t kK9Stage = 2048;                       // staging bytes per wave (1,024 records)
-static_assert(XL<9>::S == 16 * kK9Stage, "k = 9: one staging area per wave in S");
-constexpr uint64_t kK9SegMax = 20ull << 20;               // segment bytes (scratch: 2 B per byte)
+// ---------------------------------------------------------------- k = 9 classes
+// k = 9 has 131,072 canonical classes (4^9 / 2: k odd, no palindromes).  Class
+// of a 9-mer y (kf code, first base highest): its orientation whose middle base
+// is A or C, i.e. kf-code bit 9 clear -- the reverse complement flips that bit --
+// so c = bit9(y) ? rc(y) : y.  Its index is c without bit 9,
+// i = (c & 0x1FF) | (c >> 1 & 0x1FE00) (17 bits); k9_code_of(i) gives c back.
 __device__ __forceinline__ uint32_t k9_code_of(uint32_t i) { return ((i >> 9) << 10) | (i & 0x1FFu); }
-// record stream of one wave for one genome piece (wave-uniform state)
-struct K9Out {
-    uint16_t* out;    // next record slot of this wave (16-byte aligned)
-    uint32_t n;       // records written (a multiple of 8)
-    uint32_t pads;    // of which padding records (class index 0xFFFF of part 1)
-    uint32_t stage;   // LDS byte address of this wave's staging area
-};
 
 __device__ __forceinline__ uint32_t half_one(uint32_t i) { return 1u << ((i & 1u) << 4); }
 
@@ -161,9 +148,7 @@ __device__ __noinline__ void x_drain(uint32_t a, const uint32_t* __restrict__ co
             for (uint32_t h = 0; h < 2; ++h) {
                 if (!((sub >> (16 * h)) & 0xFFFFu)) continue;
                 const uint32_t bin = 2 * w + h;
-                if (K == 9) {   // part 0 (phase 1): the class of part-local index bin
-                    atomicAdd(gcounts + code2col[k9_code_of(bin)], STEP);
-                } else if (K == 8 || single) {
+                if (K == 8 || single) {
                     atomicAdd(gcounts + code2col[bin], STEP);
                 } else {
                     atomicAdd(gcounts + code2col[bin >> 2], STEP);                      // older k-mer
@@ -354,11 +339,7 @@ __device__ __forceinline__ void xc_wins8(const XcWin& x, uint32_t (&rt)[16]) {
     }
 }
 
-// ---------------------------------------------------------------- K9s, phase 1
-typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) uint16_t lds_u16;
-typedef __attribute__((address_space(3))) v4u_t lds_v4u;
-
+// ---------------------------------------------------------------- K9b, the window register
 // A region's window register for k = 9 (as xc_window): W = c | pC << (32 - 2 nl)
 // as a 64-bit value, window r = bits [2r, 2r + 18), r < 16 - nl.
 struct K9Win {
@@ -376,59 +357,6 @@ __device__ __forceinline__ K9Win k9_window(const XcCls& k, uint32_t rot) {
     x.wlo = c | ((pC << 30) & (0u - nl));   // (c's top entry is 0 after a newline)
     x.whi = pC >> (2u * nl);
     return x;
-}
-
-// The 16 windows of one lane's region (bits of R: the windows counted), every
-// class computed once: part 0 added to P (returns ORed into the result), part 1
-// staged as its 16-bit index in this wave's LDS area (slots by ballot rank, so
-// the region's records are contiguous), padded to whole 16-byte units with
-// index 0xFFFF (counted, then subtracted at the flush) and copied out to the
-// wave's record stream.  A region holds at most 1,024 part-1 windows: the
-// staging area.  The LDS reads of the copy-out precede the next region's writes
-// in the wave's LDS order.
-template <bool DENSE>
-__device__ __forceinline__ uint32_t k9_region(uint32_t wlo, uint32_t whi, uint32_t R, int lane, K9Out& so) {
-    // DENSE (fast path): windows 0..14 are counted, window 15 unless R says
-    // otherwise (a newline in the region); else R gives every window.
-    const uint32_t rlo = revpairs(whi) ^ 0xAAAAAAAAu, rhi = revpairs(wlo) ^ 0xAAAAAAAAu;
-    uint32_t n1 = 0;
-    const uint32_t sb = so.stage >> 1;   // staging slot base (u16 units)
-    // the adds' returns go to registers zeroed first and are ORed after the
-    // last window: an add under a lane test whose return were used inside the
-    // test would wait for it there (one LDS round trip per window)
-    uint32_t rt[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) rt[r] = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const uint32_t y = r < 8 ? wlo >> (2 * r) : __builtin_amdgcn_alignbit(whi, wlo, 2 * r);   // bits above 17: junk
-        const uint32_t rc = r < 8 ? rhi >> (14 - 2 * r) : __builtin_amdgcn_alignbit(rhi, rlo, 46 - 2 * r);
-        const uint32_t c = bfi((uint32_t)__builtin_amdgcn_sbfe((int)y, 9u, 1u), rc, y);   // class (18 low bits)
-        const uint32_t ki = bfi(0x1FFu, c, c >> 1);                                     // index; part at bit 16
-        const uint32_t vb = (DENSE && r < 15) ? 1u : ((R >> r) & 1u);                  // window counted
-        const uint32_t s1 = (ki >> 16) & vb;                                            // staged (part 1)
-        if (vb > s1) rt[r] = lds_add_rtn((ki << 1) & 0x1FFFCu, 1u << ((ki << 4) & 31u));
-        const uint64_t m = __builtin_amdgcn_ballot_w64(s1 != 0);
-        if (s1) {
-            const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, sb + n1));
-            *(lds_u16*)(uintptr_t)(2u * slot) = (uint16_t)ki;
-        }
-        n1 += (uint32_t)__builtin_popcountll(m);
-    }
-    uint32_t o = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o |= rt[r];
-    const uint32_t pads = (0u - n1) & 7u;
-    if ((uint32_t)lane < pads) *(lds_u16*)(uintptr_t)(so.stage + 2u * (n1 + (uint32_t)lane)) = (uint16_t)0xFFFFu;
-    const uint32_t units = (n1 + 7u) >> 3;
-    for (uint32_t u = (uint32_t)lane; u < units; u += kWave) {
-        const v4u_t x = *(lds_v4u*)(uintptr_t)(so.stage + 16u * u);
-        __builtin_nontemporal_store(x, (v4u_t*)(so.out + so.n) + u);
-    }
-    so.n += 8u * units;
-    so.pads += pads;
-    return o;
 }
 
 // ---------------------------------------------------------------- K9b (k = 9, the product)
@@ -510,11 +438,9 @@ __device__ __forceinline__ uint32_t k9b_region(uint32_t wlo, uint32_t whi, uint3
 // at most one more iteration to it before its own drain.  k = 7: at most 24 x 64
 // adds per wave and iteration, so a half stays below 0x4000 + 16 x 1536 = 0xA000;
 // k = 8: 48 x 64, below 0x2000 + 16 x 3072 = 0xE000.
-// M9 (k = 9 only): 1 = K9b (byte counters, the product), 2 = K9s (staged part 1
-// through *so; profiling builds)
-template <int K, int M9 = 1>
+template <int K>
 __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int lane, uint32_t& carry,
-                                        uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained, K9Out* so) {
+                                        uint32_t* gcounts, uint32_t& lane_total, uint32_t& drained) {
     constexpr uint32_t HOT = x_hot<K>();
     constexpr uint32_t TM = (1u << (2 * (K - 1))) - 1u;
     const XcCls k0 = xc_cls(d.q[0]), k1 = xc_cls(d.q[1]), k2 = xc_cls(d.q[2]);
@@ -522,32 +448,18 @@ __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int
     if (t_n(carry) < (uint32_t)(K - 1) || __builtin_amdgcn_ballot_w64(max(max(k0.V, k1.V), k2.V) >= kXcBad) != 0)
         return false;
     if constexpr (K == 9) {
-        // each region's window register, then its 16 windows (window 15 of a
-        // region with a newline belongs to lane L-1's region: not counted)
-        if constexpr (M9 == 1) {   // K9b: byte counters (no drains: carries are fixed as they happen)
-            const K9Win x0 = k9_window(k0, t_codes(carry));
-            uint32_t f = k9b_region<true>(x0.wlo, x0.whi, 0xFFFFu >> x0.nl, A, gcounts);
-            const K9Win x1 = k9_window(k1, wave_ror1(x0.c));
-            f |= k9b_region<true>(x1.wlo, x1.whi, 0xFFFFu >> x1.nl, A, gcounts);
-            const K9Win x2 = k9_window(k2, wave_ror1(x1.c));
-            f |= k9b_region<true>(x2.wlo, x2.whi, 0xFFFFu >> x2.nl, A, gcounts);
-            lane_total -= x0.nl + x1.nl + x2.nl;
-            carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)x2.c, kWave - 1) & TM, 31u, 31u);
-            drained |= f;
-            return true;
-        }
+        // K9b: each region's window register, then its 16 windows (window 15 of
+        // a region with a newline belongs to lane L-1's region: not counted); no
+        // drains (byte carries are corrected as they happen)
         const K9Win x0 = k9_window(k0, t_codes(carry));
-        uint32_t o = k9_region<true>(x0.wlo, x0.whi, 0xFFFFu >> x0.nl, lane, *so);
+        uint32_t f = k9b_region<true>(x0.wlo, x0.whi, 0xFFFFu >> x0.nl, A, gcounts);
         const K9Win x1 = k9_window(k1, wave_ror1(x0.c));
-        o |= k9_region<true>(x1.wlo, x1.whi, 0xFFFFu >> x1.nl, lane, *so);
+        f |= k9b_region<true>(x1.wlo, x1.whi, 0xFFFFu >> x1.nl, A, gcounts);
         const K9Win x2 = k9_window(k2, wave_ror1(x1.c));
-        o |= k9_region<true>(x2.wlo, x2.whi, 0xFFFFu >> x2.nl, lane, *so);
+        f |= k9b_region<true>(x2.wlo, x2.whi, 0xFFFFu >> x2.nl, A, gcounts);
         lane_total -= x0.nl + x1.nl + x2.nl;
         carry = tail_pack((uint32_t)__builtin_amdgcn_readlane((int)x2.c, kWave - 1) & TM, 31u, 31u);
-        if (__builtin_amdgcn_ballot_w64((o & HOT) != 0) != 0) {
-            x_scan_drain<K>(A.code2col, gcounts, lane);
-            drained = 1;
-        }
+        drained |= f;   // (K9b: a carry was corrected in the row)
         return true;
     }
     uint32_t o = 0;
@@ -585,26 +497,17 @@ __device__ __forceinline__ bool xc_fast(const XBlock& d, const CountArgs& A, int
 // Irregular 1 KiB chunk (16-byte lane layout, the general front end): every
 // counted window as a single by its forward code -- into S (k = 7) or P
 // (k = 8) -- with its return checked at once.
-template <int K, bool MASKED, int M9 = 1>
+template <int K, bool MASKED>
 __device__ __forceinline__ uint32_t x_singles(const uint4 d, const CountArgs& A, uint64_t chunk, int lane,
                                               const ChunkMask& m, uint64_t iv0, uint32_t carry, uint32_t* gcounts,
-                                              uint32_t& lane_total, uint32_t& drained, K9Out* so) {
+                                              uint32_t& lane_total, uint32_t& drained) {
     constexpr uint32_t HOT = x_hot<K>();
     uint32_t C, V, EN, ne, own;
     front_end<K, MASKED, false>(d, A, chunk, lane, m, iv0, C, V, EN, ne, own);
     const Windows win = windows<K, MASKED>(C, V, EN, ne, carry, lane);
     const uint32_t wlo = win.wlo, whi = win.whi, R = win.R;
-    if constexpr (K == 9) {   // every counted window through the k = 9 region step
-        if constexpr (M9 == 1) {   // K9b
-            drained |= k9b_region<false>(wlo, whi, R, A, gcounts);
-            lane_total += (uint32_t)__builtin_popcount(R);
-            return win.next;
-        }
-        const uint32_t o9 = k9_region<false>(wlo, whi, R, lane, *so);
-        if (__builtin_amdgcn_ballot_w64((o9 & HOT) != 0) != 0) {
-            x_scan_drain<K>(A.code2col, gcounts, lane);
-            drained = 1;
-        }
+    if constexpr (K == 9) {   // K9b: every counted window through the k = 9 region step
+        drained |= k9b_region<false>(wlo, whi, R, A, gcounts);
         lane_total += (uint32_t)__builtin_popcount(R);
         return win.next;
     }
@@ -628,9 +531,9 @@ __device__ __forceinline__ uint32_t x_singles(const uint4 d, const CountArgs& A,
 // The wave range [lo, hi) of genome [glo, ghi) in 3 KiB iterations (K1x).
 // `drained` is set if a u16 half of this range was moved to the count row (the
 // flush then adds with atomics).
-template <int K, int M9 = 1>
+template <int K>
 __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint64_t glo, uint64_t ghi, uint64_t lo,
-                                            uint64_t hi, int lane, uint32_t& drained, K9Out* so = nullptr) {
+                                            uint64_t hi, int lane, uint32_t& drained) {
     if (lo >= hi) return 0;
     uint32_t* gcounts = A.counts + (uint64_t)g * A.nbins;
     Range rg;
@@ -663,7 +566,7 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
         // one test for the whole 3 KiB (range edges, excluded intervals)
         bool fast = !rg.masked_span(A, rel, kXChunk);
         if (fast)
-            fast = xc_fast<K, M9>(bf, A, lane, carry, gcounts, lane_total, drained, so);
+            fast = xc_fast<K>(bf, A, lane, carry, gcounts, lane_total, drained);
         nfast += fast ? 1u : 0u;
         if (!fast) {
             // interval cursor before each 1 KiB third (a later test may advance it)
@@ -682,11 +585,9 @@ __device__ __forceinline__ uint32_t x_range(const CountArgs& A, int32_t g, uint6
                 // the coalesced block already holds this third in the 16-byte lane layout
                 const uint4 hb = bf.q[h];
                 if (mh)
-                    carry = x_singles<K, true, M9>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total,
-                                                   drained, so);
+                    carry = x_singles<K, true>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
                 else
-                    carry = x_singles<K, false, M9>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total,
-                                                    drained, so);
+                    carry = x_singles<K, false>(hb, A, rg.c0 + r, lane, m, ivh, carry, gcounts, lane_total, drained);
             }
         }
         rel += kXChunk;
@@ -960,203 +861,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 
     }
 }
 
-// ---------------------------------------------------------------- K9s (k = 9)
-// One pass over the bytes.  Per genome piece (a genome, or
-// its part in this workgroup's segment):
-//   phase 1  the K1x front end; every window's class once (k9_region): part 0
-//            into P, part 1 staged and copied out as 2-byte records into this
-//            workgroup's scratch (wave w at its range's offset in the piece);
-//   flush 0  part 0's columns of the row (column order, from col2rep);
-//   phase 2  each wave counts its own records into the cleared P;
-//   flush 1  part 1's columns.
-// HBM per launch: the bytes, ~1 B per window of records written and read
-// (half the windows, 2 B each), the row: ~15.6 GB on the configs[1] batch,
-// against the bucket kernel's 26.3 GB (profiles/r03/traffic_k9.json).  The
-// segments: the batch in G x ceil(total / (G x 20 MiB)) equal spans, workgroup
-// b taking spans b, b + G, ...; its scratch holds one span's records.
-
-// Phase-2 drain (part 1, 1,024 adds per wave and iteration): a u16 half at or
-// above 0x4000 moves 0x4000 at a time to the row (as x_drain; a half stays below
-// 0x4000 + 16 x 1,024 = 0x8000).
-__device__ __noinline__ void k9_drain1(uint32_t a, const uint32_t* __restrict__ code2col, uint32_t* gcounts) {
-    lds_u32* p = (lds_u32*)(uintptr_t)a;
-    uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (cur & kHot7) {
-        const uint32_t sub = ((cur & 0xC0000000u) ? (kStep7 << 16) : 0u) | ((cur & 0xC000u) ? kStep7 : 0u);
-        uint32_t seen = cur;
-        if (__hip_atomic_compare_exchange_strong(p, &seen, cur - sub, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            for (uint32_t h = 0; h < 2; ++h)
-                if ((sub >> (16 * h)) & 0xFFFFu)
-                    atomicAdd(gcounts + code2col[k9_code_of((1u << 16) | (2u * (a >> 2) + h))], kStep7);
-            cur -= sub;
-        } else {
-            cur = seen;
-        }
-    }
-}
-__device__ __noinline__ void k9_scan_drain1(const uint32_t* __restrict__ code2col, uint32_t* gcounts, int lane) {
-    for (uint32_t w = (uint32_t)lane; w < XL<9>::P / 4; w += kWave) {
-        const uint32_t v = __hip_atomic_load((lds_u32*)(uintptr_t)(4 * w), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (v & kHot7) k9_drain1(4 * w, code2col, gcounts);
-    }
-}
-
-// The 8 records of a 16-byte unit into P (part-local index: half i & 1 of word i >> 1).
-__device__ __forceinline__ uint32_t k9_add_unit(const v4u_t u) {
-    const uint32_t d[4] = {u.x, u.y, u.z, u.w};
-    uint32_t o = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        o |= lds_add_rtn((d[j] << 1) & 0x1FFFCu, 1u << ((d[j] << 4) & 16u));
-        o |= lds_add_rtn((d[j] >> 15) & 0x1FFFCu, 1u << ((d[j] >> 12) & 16u));
-    }
-    return o;
-}
-
-// Phase 2 of one wave: its n records at `rec` (n a multiple of 8), two units per
-// lane and iteration, the next iteration's loads in flight (buffer loads:
-// units past n read as zero and are not added).  Returns 1 if a half drained.
-__device__ __forceinline__ uint32_t k9_count_records(const uint16_t* rec, uint32_t n,
-                                                     const uint32_t* __restrict__ code2col, uint32_t* gcounts,
-                                                     int lane) {
-    const uint32_t U = n >> 3;
-    if (U == 0) return 0;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)rec, (short)0, (int)(16u * U), 0x00020000);
-    auto ld = [&](uint32_t u) -> v4u_t {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * u), 0, kXNt);
-        return v4u_t{v[0], v[1], v[2], v[3]};
-    };
-    const uint32_t l = (uint32_t)lane;
-    v4u_t c0 = ld(l), c1 = ld(kWave + l);
-    uint32_t drained = 0;
-    for (uint32_t b = 0; b < U; b += 2 * kWave) {
-        const v4u_t n0 = ld(b + 2 * kWave + l), n1 = ld(b + 3 * kWave + l);
-        uint32_t o = 0;
-        if (b + l < U) o |= k9_add_unit(c0);
-        if (b + kWave + l < U) o |= k9_add_unit(c1);
-        if (__builtin_amdgcn_ballot_w64((o & kHot7) != 0) != 0) {
-            k9_scan_drain1(code2col, gcounts, lane);
-            drained = 1;
-        }
-        c0 = n0, c1 = n1;
-    }
-    return drained;
-}
-
-// Flush of part `part` (1,024 threads): every column whose class is in the part,
-// in column order (coalesced row writes, half the lanes active); col2rep gives
-// the column's lexicographic representative, its class the P half.  `pads`
-// padding records were counted in part 1's index 0xFFFF.
-__device__ __forceinline__ void k9_flush(const CountArgs& A, const uint32_t* hist, uint32_t part, uint32_t* gc,
-                                         bool plain, uint32_t pads, int tid) {
-    for (uint32_t c0 = (uint32_t)tid; c0 < (1u << 17); c0 += 4 * kBlock) {
-        uint32_t rep[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rep[j] = A.col2rep[c0 + j * kBlock];   // (2^17 = 32 x 4 x kBlock)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t col = c0 + j * kBlock;
-            const uint32_t c = (rep[j] & 0x200u) ? kf_revcomp<9>(rep[j]) : rep[j];
-            if ((c >> 17) == part) {
-                const uint32_t i = ((c >> 1) & 0xFE00u) | (c & 0x1FFu);
-                uint32_t v = (hist[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu;
-                if (i == 0xFFFFu) v -= pads;   // (part 0: pads = 0)
-                if (plain)
-                    __builtin_nontemporal_store(v, gc + col);
-                else if (v)
-                    __hip_atomic_fetch_add(gc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4)))
-k9s_kernel(CountArgs A, uint16_t* scratch, uint64_t wg_records) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    {
-        uint4* h4 = (uint4*)hist;
-        for (uint32_t i = tid; i < XL<9>::bytes / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    __syncthreads();
-    if ((uint32_t)(uintptr_t)(lds_u32*)hist != 0u) __builtin_trap();   // raw LDS addresses assume base 0
-    const uint64_t base = A.goff[0];
-    const uint64_t total = A.goff[A.n_genomes] - base;
-    const uint64_t G = gridDim.x;
-    const uint64_t nseg = G * max((uint64_t)1, (total + G * kK9SegMax - 1) / (G * kK9SegMax));
-    uint16_t* wrec = scratch + (uint64_t)blockIdx.x * wg_records;
-    const uint32_t fr_lo = wave_frac((uint32_t)wave, kWaveWeights), fr_hi = wave_frac((uint32_t)wave + 1, kWaveWeights);
-    uint32_t* slots = hist + XL<9>::P / 4;   // after phase 1: 16 drain flags, 16 pad counts, 16 drain flags
-    for (uint64_t sg = blockIdx.x; sg < nseg; sg += G) {
-        const uint64_t span_lo = base + ((total / nseg * sg + (total % nseg) * sg / nseg) & ~(uint64_t)15);
-        const uint64_t span_hi = sg + 1 == nseg ? base + total
-                                                : base + ((total / nseg * (sg + 1) + (total % nseg) * (sg + 1) / nseg) &
-                                                          ~(uint64_t)15);
-        if (span_lo >= span_hi) continue;
-        int32_t g = (int32_t)wave_upper_bound((uint64_t)A.n_genomes, span_lo, lane,
-                                              [&](uint64_t i) { return A.goff[i + 1]; });
-        for (; g < A.n_genomes; ++g) {
-            __builtin_amdgcn_s_setprio(3);
-            const uint64_t glo = A.goff[g], ghi = A.goff[g + 1];
-            if (glo >= span_hi) break;
-            const uint64_t plo = max(glo, span_lo), phi = min(ghi, span_hi);
-            if (phi <= plo) continue;
-            const uint64_t lo = split_at_frac(plo, phi, fr_lo), hi = split_at_frac(plo, phi, fr_hi);
-            K9Out so;
-            so.out = wrec + ((lo & ~(uint64_t)15) - (plo & ~(uint64_t)15));
-            so.n = 0;
-            so.pads = 0;
-            so.stage = XL<9>::P + (uint32_t)wave * kK9Stage;
-            uint32_t drained0 = 0;
-            unsigned long long s = x_range<9, 2>(A, g, glo, ghi, lo, hi, lane, drained0, &so);
-            __builtin_amdgcn_s_setprio(0);
-            uint32_t* gc = A.counts + (uint64_t)g * A.nbins;
-            uint32_t* gcounts = gc;
-            const bool whole = plo == glo && phi == ghi && !(A.flags & KF_ACCUMULATE);
-            // every wave's adds, staging and record stores are done (its own
-            // records are read back by the same wave in phase 2)
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (lane == 0) {
-                slots[wave] = drained0;
-                slots[16 + wave] = so.pads;
-            }
-            lds_barrier();
-            uint32_t any0 = 0, pads = 0;
-#pragma unroll
-            for (int w = 0; w < 16; ++w) {
-                any0 |= slots[w];
-                pads += slots[16 + w];
-            }
-            k9_flush(A, hist, 0, gc, whole && !any0, 0, tid);
-            lds_barrier();   // P read
-            {
-                uint4* h4 = (uint4*)hist;
-                for (uint32_t i = tid; i < XL<9>::P / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
-            }
-            lds_barrier();
-            const uint32_t drained1 = k9_count_records(so.out, so.n, A.code2col, gcounts, lane);
-            if (lane == 0) slots[32 + wave] = drained1;
-            lds_barrier();
-            uint32_t any1 = 0;
-#pragma unroll
-            for (int w = 0; w < 16; ++w) any1 |= slots[32 + w];
-            k9_flush(A, hist, 1, gc, whole && !any1, pads, tid);
-            lds_barrier();   // P read
-            {
-                uint4* h4 = (uint4*)hist;
-                for (uint32_t i = tid; i < XL<9>::P / 16; i += kBlock) h4[i] = make_uint4(0u, 0u, 0u, 0u);
-            }
-            s = wave_sum(s);
-            if (lane == 0 && s) atomicAdd(A.totals + g, s);
-            lds_barrier();   // P zero before the next piece's adds
-        }
-    }
-}
-
 // ---------------------------------------------------------------- synthetic input
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -1307,10 +1011,6 @@ int lds_bytes_for(int k) {
     }
 }
 
-// k = 9: records scratch per workgroup (one segment's bytes, 2 B each, plus the
-// wave ranges' 16-byte alignment) and its total for `grid` workgroups
-constexpr uint64_t kK9WgRecords = kK9SegMax + 1024;
-[[maybe_unused]] uint64_t k9_scratch_bytes(int grid) { return (uint64_t)grid * kK9WgRecords * 2; }
 
 // grid per (k, device): workgroups per CU from the occupancy API x CUs
 int g_grid[KF_MAX_K + 1][64];
@@ -1371,7 +1071,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     hipStream_t s = (hipStream_t)stream;
 #ifdef KF_PROFILE_BUILD
     // profiling builds: KF_K9_BUCKET=1 counts k = 9 with bucket_kernel<9> (the
-    // rounds 1-5 path), for A/B against K9s
+    // rounds 1-5 path), for A/B against K9b
     const bool bucket = k >= 10 || (k == 9 && getenv("KF_K9_BUCKET") && atoi(getenv("KF_K9_BUCKET")));
 #else
     const bool bucket = k >= 10;
@@ -1398,23 +1098,7 @@ extern "C" int kf_count_batch(const uint8_t* d_bytes, const uint64_t* d_goff, in
     int grid = 0, block = 0, lds = 0;
     const int rc = launch_info(k, &grid, &block, &lds);
     if (rc) return rc;
-#ifdef KF_PROFILE_BUILD
-    // profiling builds: KF_K9_STAGED=1 counts k = 9 with K9s (half the classes
-    // staged to HBM; round 6's first k = 9 kernel), for A/B against K9b
-    if (k == 9 && getenv("KF_K9_STAGED") && atoi(getenv("KF_K9_STAGED"))) {
-        if (hipFuncSetAttribute((const void*)&k9s_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-            hipSuccess)
-            return kf_fail(KF_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-        return scratch_launch(k9_scratch_bytes(grid), s, [&](void* scratch) {
-            uint16_t* rec = (uint16_t*)scratch;
-            uint64_t wg = kK9WgRecords;
-            void* args9[] = {&A, &rec, &wg};
-            if (hipLaunchKernel((void*)&k9s_kernel, dim3(grid), dim3(block), args9, (size_t)lds, s) != hipSuccess)
-                return kf_fail(KF_EHIP, "k=9 count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-            return (int)KF_OK;
-        });
-    }
-#endif
+
     void* args[] = {&A};
     if (hipLaunchKernel(kernel_for(k), dim3(grid), dim3(block), args, (size_t)lds, s) != hipSuccess)
         return kf_fail(KF_EHIP, "count kernel launch failed: %s", hipGetErrorString(hipGetLastError()));

@@ -6,8 +6,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <functional>
-
 namespace kf {
 
 constexpr int kWave = 64;
@@ -558,11 +556,5 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 int bucket_launch(const CountArgs& A, int k, uint32_t flags, hipStream_t s);
 int bucket_launch_info(int k, int* grid, int* block, int* lds);
 int bucket_reserve(int k, int32_t max_genomes);
-// The device's shared scratch (kf_bucket.hip), used by the bucket kernels and by
-// k = 9's record stream: grown to at least `bytes` (a regrowth synchronises the
-// device); scratch_launch runs `launch(ptr)` after the previous user of the
-// scratch on any stream, and orders later users after it.
-int scratch_reserve(size_t bytes);
-int scratch_launch(size_t bytes, hipStream_t s, const std::function<int(void*)>& launch);
 
 }  // namespace kf

@@ -504,9 +504,10 @@ def test_pair_counter_u16_drains_low_complexity(torch_dev, oracle, k):
 
 
 def _k9_part1_walk(rng, n):
-    """A sequence whose 9-mers are mostly in K9s's part 1 (class first base T or
-    G): each next base is drawn among those that keep the window in part 1 when
-    any does (about 2/3 of the windows end up there)."""
+    """A sequence whose 9-mers' classes mostly start with T or G (the upper half
+    of the class indices; round 6's first k = 9 kernel, K9s in tools/zoo, staged
+    exactly those): each next base is drawn among those that keep the window
+    there when any does (about 2/3 of the windows end up there)."""
     y = np.arange(1 << 18, dtype=np.uint32)   # kf code A0 C1 T2 G3
     rc, t = np.zeros_like(y), y.copy()
     for _ in range(9):
@@ -523,11 +524,10 @@ def _k9_part1_walk(rng, n):
 
 
 def test_k9_staged_part1_heavy_and_periodic(torch_dev, oracle):
-    """K9s (k = 9, one pass): part-1-heavy sequence (regions with more than 512
-    staged records: two copy-out rounds), short lines and records (the irregular
-    path stages too), and periodic sequence whose few classes overflow the u16
-    halves in both phases (phase-1 and phase-2 drains, and the padding records'
-    class 0xFFFF of part 1 = GGGGAGGGG... mixed in).  kf2vec/main.py:293-294."""
+    """k = 9 (K9b byte counters): sequence concentrated on the upper half of the
+    classes, short lines and records (the irregular path), and periodic sequence
+    whose few classes wrap their u8 counters thousands of times (the class
+    index 0xFFFF, GGGGAGGGG, mixed in).  kf2vec/main.py:293-294."""
     rng = np.random.default_rng(909)
     walk = _k9_part1_walk(rng, 400_000)
     blobs = [b">w\n" + gen.wrap(walk, 80),
@@ -559,10 +559,10 @@ def test_k9_byte_counter_carry_chains(torch_dev, oracle):
 
 
 def test_k9_two_segments_every_genome(torch_dev, oracle):
-    """K9s splits a batch into G x ceil(total / (G x 20 MiB)) segments: 1,200 x 5
-    Mbp (6.07 GB, N runs) gives every workgroup two, so its record scratch is
-    reused and genomes straddle segment boundaries (atomic flushes).  Every
-    genome's row and total bit-exact against the oracle."""
+    """k = 9 at full size past configs[1]: 1,200 x 5 Mbp (6.07 GB, N runs) in one
+    launch, so every workgroup span holds ~5 genome pieces and ~250 genomes
+    straddle two spans (atomic flushes).  Every genome's row and total bit-exact
+    against the oracle (kf2vec/main.py:293-294, 309-323)."""
     import torch
     from kf2vecfsw_amd import counter as C
     from test_gpu_configs import host_threads
