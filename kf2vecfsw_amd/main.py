@@ -355,9 +355,15 @@ def get_frequencies(args) -> None:
         return hb
 
     # Three-stage pipeline over batches:
-    #   readers (2)   : read batches i+1, i+2 into pinned memory (one shared pool
-    #                   of -p file workers keeps all cores busy) and put each on
-    #                   the copy stream as soon as it is read
+    #   readers (2)   : read the next batches into pinned memory (one shared pool
+    #                   of host-thread file workers keeps all cores busy) and put
+    #                   each on the copy stream as soon as it is read; as many
+    #                   batches are queued for them as there are pinned slots, so
+    #                   the reads (and the copies behind them) run back to back
+    #                   whatever this thread is doing (r06 KF_TRACE: with only
+    #                   the next two queued, the third read started when this
+    #                   thread took batch 0, after its ~2.5 ms of set-up, and the
+    #                   copy stream idled 1.5 ms)
     #   this thread   : record index + count + D2H of batch i on a side stream
     #   writer thread : wait for batch i's copy-back, format + write its .kf files
     # The prints stay in the reference's per-file order (main.py:332-341).
@@ -366,7 +372,8 @@ def get_frequencies(args) -> None:
     depth = int(os.environ.get("KF_READ_AHEAD", "2"))   # batches being read ahead
     reader = ThreadPoolExecutor(max_workers=depth)
     writer = ThreadPoolExecutor(max_workers=1)
-    reads = deque(reader.submit(pack, i, batches[i]) for i in range(min(depth, len(batches))))
+    ahead = n_slots   # batches queued for the readers (read, or copied, but not yet counted)
+    reads = deque(reader.submit(pack, i, batches[i]) for i in range(min(ahead, len(batches))))
     # While the first batches are read: the side stream's first event and launch
     # and the device block for a batch (the caching allocator keeps it for this
     # stream) would otherwise cost ~2 ms between the first read and its H2D
@@ -399,8 +406,8 @@ def get_frequencies(args) -> None:
         hb = reads.popleft().result()
         if trace:
             tr.append(("got", bi, t_wait, now_ms()))
-        if bi + depth < len(batches):
-            reads.append(reader.submit(pack, bi + depth, batches[bi + depth]))
+        if bi + ahead < len(batches):   # its slot is batch bi's, free once bi's copy has run
+            reads.append(reader.submit(pack, bi + ahead, batches[bi + ahead]))
         with torch.cuda.stream(stream):
             if trace:
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
