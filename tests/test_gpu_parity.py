@@ -88,7 +88,7 @@ def test_random_fasta_all_k(torch_dev, oracle, k):
     check_against_oracle(oracle, blobs, k, counts, totals, tag="rand")
 
 
-@pytest.mark.parametrize("k", [3, 7, 8, 11])
+@pytest.mark.parametrize("k", [3, 7, 8, 9, 11])
 def test_unaligned_genome_offsets(torch_dev, oracle, k):
     """Genome boundaries at arbitrary byte offsets (not 16-aligned) and genomes
     smaller than one lane block / one chunk."""
@@ -171,7 +171,7 @@ def test_device_synth_matches_oracle_and_counts(torch_dev, oracle):
                 assert t == L - 7 + 1
 
 
-@pytest.mark.parametrize("k", [7, 11])
+@pytest.mark.parametrize("k", [7, 9, 11])
 def test_deterministic_and_accumulate(torch_dev, oracle, k):
     import torch
     from kf2vecfsw_amd import counter as C
@@ -556,6 +556,15 @@ def test_k9_byte_counter_carry_chains(torch_dev, oracle):
              b">few\n" + gen.wrap(gen.random_seq(rng, 30_000), 80)]
     counts, totals = run_batch(blobs, 9, torch_dev)
     check_against_oracle(oracle, blobs, 9, counts, totals, tag="k9b")
+    # KF_ACCUMULATE: the corrections and the byte flush add onto rows that hold counts
+    import torch
+    from kf2vecfsw_amd import counter as C
+    db = C.to_device(C.pack_genomes(blobs), torch_dev)
+    kc = counter(9, torch_dev)
+    a, ta = kc.count(db)
+    kc.count(db, a, ta, accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(C.counts_to_numpy(a), 2 * counts) and np.array_equal(ta.cpu().numpy(), 2 * totals)
 
 
 def test_k9_two_segments_every_genome(torch_dev, oracle):
