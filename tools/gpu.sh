@@ -62,7 +62,7 @@ for step in "$@"; do
             ENV:*) envs=("${v#ENV:}"); lib=kf2vecfsw_amd/libkf2vec_gpu_ablation.so ;;
             *) lib=kf2vecfsw_amd/libkf2vec_gpu_$v.so ;;
           esac
-          run 150 "$OUT/alt_p.json" env ${lib:+KF2VEC_GPU_LIB=$REPO/$lib} "${envs[@]}" \
+          run 150 "$OUT/alt_p.json" env ${lib:+KF2VEC_ALLOW_FOREIGN_LIB=1 KF2VEC_GPU_LIB=$REPO/$lib} "${envs[@]}" \
             python3 -u tools/r04_run.py --k "$ak" --reps "$areps"
           python3 -c "import json,statistics,sys;x=json.loads(open('$OUT/alt_p.json').read().strip().splitlines()[-1]);print(json.dumps({'variant':sys.argv[1],'k':$ak,'median_ms':statistics.median(x['ms'][2:]),'ms':x['ms'],'ok':x.get('totals_analytic')}))" "$v" >> "$OUT/alt_$n.jsonl"
         done
