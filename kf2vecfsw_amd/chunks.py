@@ -131,6 +131,13 @@ class Genome:
     starts: np.ndarray | None = None
     excluded: str | None = None       # "none" (no contig >= 10 kbp) or "few"
     write: bool = True                # False: a later file has the same sample name
+    # a file counted in record-aligned parts (main.record_pieces): its parts'
+    # rows go to out_name, appended after the first part (cont); only the last
+    # part is reported, with the file's windows (total_windows)
+    out_name: str | None = None
+    cont: bool = False
+    last: bool = True
+    total_windows: int | None = None
 
     @property
     def n_windows(self) -> int:
@@ -143,6 +150,19 @@ class Genome:
             return []
         return [self.prefixes[int(p)] + "{}-{}".format(int(s) + 1, int(s) + CHUNK_SZ)
                 for p, s in zip(self.wpre, self.wpos)]
+
+
+def shadow(genomes: list[Genome]) -> None:
+    """The reference writes genome by genome, so a later file with the same
+    sample name replaces an earlier one's .kf: inside a batch, only the last
+    written one is counted (across batches the in-order writer does it).  Only a
+    file's last part decides: its earlier parts go to its side file anyway."""
+    kept = set()
+    for gm in reversed(genomes):
+        gm.write = True
+        if gm.excluded is None and gm.last:
+            gm.write = gm.sample not in kept
+            kept.add(gm.sample)
 
 
 class ChunkPipeline:
@@ -227,14 +247,7 @@ class ChunkPipeline:
                 gm.excluded = "none"                               # main.py:761-778
             elif gm.n_windows < CHUNK_CNT_THR:
                 gm.excluded = "few"                                # main.py:845-860
-        # the reference writes genome by genome, so a later file with the same
-        # sample name replaces an earlier one's .kf: inside a batch, only the last
-        # written one is counted (across batches the in-order writer does it)
-        kept = set()
-        for gm in reversed(genomes):
-            if gm.excluded is None:
-                gm.write = gm.sample not in kept
-                kept.add(gm.sample)
+        shadow(genomes)
         _tr("plan", t0, windows=sum(g.n_windows for g in genomes))
         return d_out
 
@@ -284,8 +297,8 @@ class ChunkPipeline:
                 a, b = max(int(row0[gi]), w0), min(int(row0[gi + 1]), w1)
                 if a >= b:
                     continue
-                segs.append((os.path.join(output_dir, "{}.kf".format(g.sample)), a - w0, b - w0, g,
-                             a - int(row0[gi]), a > int(row0[gi])))
+                segs.append((os.path.join(output_dir, g.out_name or "{}.kf".format(g.sample)), a - w0, b - w0, g,
+                             a - int(row0[gi]), g.cont or a > int(row0[gi])))
             args = self._write_args(segs)   # built here: the writer thread only formats + writes
             if len(self.pending) >= 2:      # at most two launches queued for the writer
                 self.pending.pop(0).result()
@@ -302,9 +315,14 @@ class ChunkPipeline:
         t0 = time.perf_counter()
         if not segs:
             return None
-        paths = (ctypes.c_char_p * len(segs))(*[os.fsencode(s[0]) for s in segs])
-        row0 = np.asarray([0] + [s[2] for s in segs], dtype=np.int32)
-        app = np.asarray([1 if s[5] else 0 for s in segs], dtype=np.uint8)
+        # consecutive segments of one file (the parts of a file counted in
+        # record-aligned parts) are one native segment: the writer opens each
+        # segment's file once and lays its rows out from the file's end
+        first = [i for i in range(len(segs)) if i == 0 or segs[i][0] != segs[i - 1][0]]
+        ends = [segs[j - 1][2] for j in first[1:]] + [segs[-1][2]]
+        paths = (ctypes.c_char_p * len(first))(*[os.fsencode(segs[i][0]) for i in first])
+        row0 = np.asarray([0] + ends, dtype=np.int32)
+        app = np.asarray([1 if segs[i][5] else 0 for i in first], dtype=np.uint8)
         pre, rpre, rpos = [], [], []
         for _, a, b, g, o, _ap in segs:
             rpre.append(g.wpre[o: o + (b - a)].astype(np.uint32) + len(pre))
@@ -315,7 +333,7 @@ class ChunkPipeline:
         enc = [x.encode(errors="surrogateescape") for x in pre]
         arr = (ctypes.c_char_p * len(enc))(*enc)
         _tr("encode_names", t0, rows=int(rpos.size))
-        return (len(segs), paths, row0, app, enc, arr, rpre, rpos)
+        return (len(first), paths, row0, app, enc, arr, rpre, rpos)
 
     def _write(self, ev, host: torch.Tensor, args) -> None:
         """Format + write one launch's rows, once its counts are on the host."""
@@ -333,6 +351,13 @@ class ChunkPipeline:
                                                rows.shape[1], int(self.pseudocount), 1, self.threads),
                 "kf_write_kf_segments16")
         _tr("format_write", t0, segs=n_seg)
+
+    def after_writes(self, fn):
+        """Run fn on the writer thread once every write queued so far is done
+        (the writer runs in order); returns its future."""
+        f = self.writer.submit(fn)
+        self.pending.append(f)
+        return f
 
     def drain(self) -> None:
         """Wait for every queued write."""

@@ -187,11 +187,12 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
 
 
 def pack_ranges(ranges: Sequence[tuple[str, int, int]], names: Sequence[str] | None = None, pin: bool = True,
-                threads: int = 8, chunk: int = 64 << 20) -> HostBatch:
+                threads: int = 8, chunk: int = 64 << 20, index: bool = False) -> HostBatch:
     """As pack_files for byte ranges [(path, start, end)] of files (the pieces of
-    a file too large for one sparse call, main.fasta_pieces), read by os.preadv
-    in chunks of `chunk` bytes on `threads` threads; FASTA only (the record index
-    is left to the device)."""
+    a file too large for one sparse call, main.fasta_pieces, or get_chunks'
+    record-aligned parts, main.record_pieces), read by os.preadv in chunks of
+    `chunk` bytes on `threads` threads; FASTA only (index=False: the record index
+    is left to the device; index=True: the header lines indexed here)."""
     from concurrent.futures import ThreadPoolExecutor
     sizes = [e - a for _, a, e in ranges]
     off = _layout(sizes)
@@ -219,7 +220,12 @@ def pack_ranges(ranges: Sequence[tuple[str, int, int]], names: Sequence[str] | N
 
     with ThreadPoolExecutor(max_workers=max(1, int(threads))) as ex:
         list(ex.map(read, jobs))
-    return HostBatch(data, off, None, list(names) if names else [f"{p}:{a}" for p, a, _ in ranges])
+        excl = None
+        if index:
+            parts = list(ex.map(lambda i: index_records(d[int(off[i]): int(off[i]) + sizes[i]], N.KF_FMT_FASTA,
+                                                        int(off[i]))[0], range(len(ranges))))
+            excl = (np.concatenate(parts) if parts else np.zeros(0, np.uint64)).astype(np.uint64)
+    return HostBatch(data, off, excl, list(names) if names else [f"{p}:{a}" for p, a, _ in ranges])
 
 
 @dataclasses.dataclass

@@ -95,9 +95,13 @@ def _batches(paths: list[str], budget: int, ramp: bool = False, max_files: int |
     that alone) and at most `max_files` files.  ramp: the first two batches get a
     quarter and a half of the byte budget, so a pipeline's later stages start
     sooner."""
+    return _size_batches([os.path.getsize(p) for p in paths], budget, ramp, max_files)
+
+
+def _size_batches(sizes: list[int], budget: int, ramp: bool = False, max_files: int | None = None) -> list[list[int]]:
+    """_batches over item sizes (files, or get_chunks' file parts)."""
     out, cur, size = [], [], 0
-    for i, p in enumerate(paths):
-        s = os.path.getsize(p)
+    for i, s in enumerate(sizes):
         lim = budget >> max(0, 2 - len(out)) if ramp else budget
         if cur and (size + s > lim or (max_files is not None and len(cur) >= max_files)):
             out.append(cur)
@@ -556,12 +560,10 @@ MAX_CALL_BYTES = (1 << 32) - 1   # kf_sparse_count / kf_chunk_compact: 32-bit of
 
 
 def _refuse_huge_files(paths: list[str], what: str) -> None:
-    """The sparse counter and the get_chunks pre-pass take one genome per call
-    slice with 32-bit offsets: a single input file of 4 GiB or more is refused
-    up front (before any output is written), not partway through a directory
-    (ADVICE r04).  The reference's Jellyfish/seqtk pipeline has no such limit;
-    the largest assembled genomes in kf2vec's domain (bacterial/archaeal, a few
-    Mbp) are three orders of magnitude below it."""
+    """The sparse counter takes one genome per call slice with 32-bit offsets:
+    a FASTQ file of 4 GiB or more (get_kmers -k 13..31 cuts only FASTA files into
+    pieces) is refused up front, before any output is written, not partway
+    through a directory."""
     big = [p for p in paths if os.path.getsize(p) > MAX_CALL_BYTES - 16]
     if big:
         raise ValueError("{}: input file(s) of 4 GiB or more are not supported (per-call 32-bit offsets): {}".format(
@@ -649,6 +651,47 @@ def fasta_pieces(path: str, k: int, piece: int = SPLIT_BYTES) -> list[tuple[int,
                 for i, c in enumerate(cuts)]
     finally:
         os.close(fd)
+
+
+def _next_record(fd: int, pos: int, size: int) -> int:
+    """Offset of the first header line ('>' at a line start) at or after pos
+    (pos > 0), or size if there is none."""
+    step = 1 << 20
+    q = pos - 1                       # the byte before pos: a '\n' there makes pos a line start
+    while q < size:
+        blk = os.pread(fd, min(step, size - q), q)
+        j = blk.find(b"\n>")
+        if j >= 0:
+            return q + j + 1
+        if len(blk) < 2:
+            return size
+        q += len(blk) - 1             # (a "\n>" across the block edge)
+    return size
+
+
+def record_pieces(path: str, piece: int | None = None) -> list[tuple[int, int]]:
+    """Byte ranges [(a_i, e_i)] that cut a FASTA file into parts of about
+    `piece` bytes at record starts (header lines), so every part holds whole
+    records: get_chunks' windows never span a record, so its parts are counted
+    independently (a part's rows follow the previous part's, in file order).
+    Bytes before the first header stay in part 0 (no record: seqtk skips them).
+    A single record longer than `piece` stays whole.  The reference's
+    seqtk/seqkit chain reads a file of any size (kf2vec/main.py:726-760)."""
+    piece = SPLIT_BYTES if piece is None else piece
+    size = os.path.getsize(path)
+    if size <= piece:
+        return [(0, size)]
+    cuts = [0]
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        while True:
+            c = _next_record(fd, cuts[-1] + piece, size)
+            if c >= size:
+                break
+            cuts.append(c)
+    finally:
+        os.close(fd)
+    return [(c, cuts[i + 1] if i + 1 < len(cuts) else size) for i, c in enumerate(cuts)]
 
 
 def _merge_sorted_counts(parts: list) -> tuple:
@@ -802,7 +845,7 @@ def get_chunks(args) -> None:
     import time
 
     from . import chunks as CH
-    from .counter import KmerCounter, pack_files
+    from .counter import KmerCounter, pack_files, pack_ranges
 
     CH.TRACE = os.environ.get("KF_TRACE") == "1"
     since = time.time()
@@ -841,25 +884,86 @@ def get_chunks(args) -> None:
     threads = host_threads(args.p)
     pipe = CH.ChunkPipeline(counter, device, max_windows, threads, args.pseudocount)
     paths = [os.path.join(args.input_dir, f) for f in files_names]
-    _refuse_huge_files(paths, "get_chunks (kf_chunk_compact)")
-    # input batches of files: about a quarter of the input each (the first two
+    # units: whole files, or the record-aligned parts of a file above SPLIT_BYTES
+    # (each part below kf_chunk_compact's 32-bit offsets; a single record of 4 GiB
+    # or more is refused before anything is written)
+    units = []   # (file index, start, end, part, parts)
+    for fi, p in enumerate(paths):
+        pcs = record_pieces(p)
+        for j, (a, e) in enumerate(pcs):
+            if e - a > MAX_CALL_BYTES - 16:
+                raise ValueError("get_chunks (kf_chunk_compact): a FASTA record of 4 GiB or more is not supported "
+                                 "(per-call 32-bit offsets): {} at byte {}".format(files_names[fi], a))
+            units.append((fi, a, e, j, len(pcs)))
+    # input batches of units: about a quarter of the input each (the first two
     # smaller, so the writer starts sooner), so that reading and preparing one
     # batch overlaps writing the previous one, within the budget (and below 4 GiB
     # of processed sequence: kf_chunk_compact's offsets)
-    total_in = sum(os.path.getsize(p) for p in paths)
-    batches = _batches(paths, min(budget, 3 << 30, max(total_in // 4, 16 << 20)), ramp=True)
+    usz = [e - a for _, a, e, _, _ in units]
+    batches = _size_batches(usz, min(budget, 3 << 30, max(sum(usz) // 4, 16 << 20)), ramp=True)
     files_pool = ThreadPoolExecutor(max_workers=threads)
     reader = ThreadPoolExecutor(max_workers=1)
 
     def read(idx):
         t0 = time.perf_counter()
-        hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], fmt=N.KF_FMT_FASTA,
-                        pool=files_pool)
+        us = [units[u] for u in idx]
+        names = [samples_names[fi] for fi, _, _, _, _ in us]
+        if all(n == 1 for *_, n in us):
+            hb = pack_files([paths[fi] for fi, *_ in us], names, fmt=N.KF_FMT_FASTA, pool=files_pool)
+        else:
+            hb = pack_ranges([(paths[fi], a, e) for fi, a, e, _, _ in us], names, threads=threads, index=True)
         CH._tr("read", t0, files=len(idx))
         return hb
 
+    # a file in several parts: windows and long contigs so far; written to a
+    # side file that replaces <sample>.kf after its last part (or is removed if
+    # the file is excluded or a later file of the same name replaces it)
+    acc: dict = {}
+
+    def settle(genomes, us):
+        """The parts' exclusions and names; returns the side-file steps for the
+        writer: (before this batch's rows) a stale side file of a file whose first
+        part is here removed, (after them) the move of a file whose last part is."""
+        lasts, first = [], []
+        for gm, (fi, _a, _e, j, n) in zip(genomes, us):
+            if n == 1:
+                continue
+            if j == 0:
+                first.append(os.path.join(args.output_dir, "{}.kf.parts".format(gm.sample)))
+            nw, longc = acc.get(fi, (0, False))
+            nw, longc = nw + gm.n_windows, longc or gm.n_windows > 0
+            acc[fi] = (nw, longc)
+            gm.out_name = "{}.kf.parts".format(gm.sample)
+            gm.cont, gm.last = j > 0, j == n - 1
+            if not gm.last:
+                gm.excluded = None    # decided by the last part
+                continue
+            gm.total_windows = nw
+            gm.excluded = "none" if not longc else ("few" if nw < CH.CHUNK_CNT_THR else None)
+            lasts.append(gm)
+        CH.shadow(genomes)
+        moves = []
+        for gm in lasts:
+            side = os.path.join(args.output_dir, gm.out_name)
+            final = os.path.join(args.output_dir, "{}.kf".format(gm.sample))
+
+            def move(side=side, final=final, keep=gm.excluded is None and gm.write):
+                if keep:
+                    os.replace(side, final)
+                elif os.path.exists(side):
+                    os.remove(side)
+            moves.append(move)
+
+        def clear(paths=first):
+            for p in paths:
+                if os.path.exists(p):
+                    os.remove(p)
+        return clear, moves
+
     def report(genomes):
         for gm in genomes:
+            if not gm.last:
+                continue
             log.info("\n==> Start processing. Sample: {}".format(gm.fname))                   # main.py:703
             log.info(">>> Formatting to single line. Sample: {}".format(gm.fname))            # :728
             log.info(">>> Replacing stretches of N. Sample: {}".format(gm.fname))             # :737
@@ -872,7 +976,7 @@ def get_chunks(args) -> None:
             log.info(">>> Computing contig statistics. Sample: {}".format(gm.fname))          # :799
             if gm.excluded == "few":                                                          # :845-860
                 stamp("\n==> Excluded {}. {} chunks is too low. {} is required.".format(
-                    gm.fname, gm.n_windows, CH.CHUNK_CNT_THR))
+                    gm.fname, gm.n_windows if gm.total_windows is None else gm.total_windows, CH.CHUNK_CNT_THR))
                 continue
             stamp("\n==> Done chunk processing for {}.".format(gm.fname))                    # :866
             # the reference runs get_frequencies on the genome's chunk directory here
@@ -890,10 +994,13 @@ def get_chunks(args) -> None:
         CH._tr("wait_read", t0, batch=bi)
         if bi + 1 < len(batches):
             nxt = reader.submit(read, batches[bi + 1])
-        genomes = [CH.Genome(files_names[i], samples_names[i]) for i in idx]
+        genomes = [CH.Genome(files_names[units[u][0]], samples_names[units[u][0]]) for u in idx]
         d_seq = pipe.prepare(hb, genomes)
+        clear, moves = settle(genomes, [units[u] for u in idx])
         t0 = time.perf_counter()
+        pipe.after_writes(clear)
         futs = pipe.count_and_write(d_seq, genomes, args.output_dir)
+        futs += [pipe.after_writes(f) for f in moves]   # in the writer's order: before the next batch's writes
         CH._tr("issue_counts", t0, launches=len(futs))
         del hb, d_seq
         if prev is not None:

@@ -49,3 +49,14 @@ def oracle():
     import kf_oracle
     kf_oracle.build()
     return kf_oracle
+
+
+@pytest.fixture(autouse=True)
+def _stall_dump():
+    """A test that runs past KF_TEST_STALL_S seconds (170: before a 3-minute
+    silence watchdog) dumps every thread's stack and ends the run, so a stall
+    names its test and the line it waits on instead of ending silently."""
+    import faulthandler
+    faulthandler.dump_traceback_later(int(os.environ.get("KF_TEST_STALL_S", "170")), exit=True)
+    yield
+    faulthandler.cancel_dump_traceback_later()

@@ -847,6 +847,103 @@ def test_cli_get_chunks_multicontig_vs_oracle(torch_dev, oracle, tmp_path):
             assert f.read_text() == exp, name
 
 
+def test_cli_get_chunks_record_parts_equal_whole_files(torch_dev, oracle, tmp_path, monkeypatch):
+    """get_chunks with every file above SPLIT_BYTES (here 30 kB) cut into
+    record-aligned parts (main.record_pieces): the output
+    directory and the log lines are the same as with whole files, byte for byte
+    (times aside).  Cases: multi-contig genomes, a split genome with fewer than 5
+    windows in all ("few") and one with no contig >= 10 kbp ("none"), each across
+    parts, and two sample names shared by a split and an unsplit file (the later
+    file in listdir order wins, main.py:357).  Rows are also checked against the
+    oracle's windows for the kept genomes."""
+    import re
+    from kf2vecfsw_amd import main as M
+    rng = np.random.default_rng(7070)
+    inp = tmp_path / "in"
+    inp.mkdir()
+    short = lambda n: b"".join(b">s%d\n" % i + gen.wrap(gen.random_seq(rng, 9000), 80) for i in range(n))
+    files = {f"g{i}.fna": _chunk_genome(rng, int(rng.integers(3, 10))) for i in range(5)}
+    files["few.fna"] = short(4) + b">long\n" + gen.wrap(gen.random_seq(rng, 21000), 60) + short(3)
+    files["none.fna"] = short(8)
+    files["dupa.fna"] = _chunk_genome(rng, 8)
+    files["dupa.fa"] = b">d\n" + gen.wrap(gen.random_seq(rng, 70000), 70)
+    files["dupb.fna"] = b">d\n" + gen.wrap(gen.random_seq(rng, 61000), 70)
+    files["dupb.fa"] = _chunk_genome(rng, 8)
+    for name, b in files.items():
+        (inp / name).write_bytes(b)
+    assert sum(len(M.record_pieces(str(inp / f), 30000)) > 1 for f in files) >= 6
+
+    def run(tag):
+        out = tmp_path / tag
+        out.mkdir()
+        M.main(["get_chunks", "-input_dir", str(inp), "-output_dir", str(out), "-k", "7"])
+        logs = {f.name: re.sub(r"Time: \d\d:\d\d:\d\d", "", f.read_text()) for f in out.glob("*.log")}
+        return {f.name: f.read_bytes() for f in out.iterdir() if f.suffix != ".log"}, logs
+
+    whole, wlog = run("whole")
+    monkeypatch.setattr(M, "SPLIT_BYTES", 30000)
+    parts, plog = run("parts")
+    assert sorted(parts) == sorted(whole) and "few.kf" not in parts and "none.kf" not in parts
+    for f in whole:
+        assert parts[f] == whole[f], f
+    assert plog == wlog
+    order, samples = M.list_inputs(str(inp))
+    for f, smp in zip(order, samples):
+        if order[[i for i, x in enumerate(samples) if x == smp][-1]] != f:
+            continue   # an earlier file of a shared name
+        wins = oracle.chunk_windows(files[f], smp)
+        if len(wins) < 5:
+            assert smp + ".kf" not in parts, f
+            continue
+        exp = "".join(oracle.kf_line(n, oracle.count(b">w\n" + w + b"\n", 7)[0], raw_cnt=True) for n, w in wins)
+        assert parts[smp + ".kf"].decode() == exp, f
+
+
+def test_cli_get_chunks_file_above_4gib(torch_dev, oracle, tmp_path):
+    """get_chunks on ONE ~4.4 GB FASTA, past kf_chunk_compact's 32-bit offsets
+    (the reference's seqtk/seqkit chain takes any size,
+    kf2vec/main.py:726-760): the file is counted in record-aligned 1 GiB parts.
+    It is ~480,000 records of 9 kbp (below the 10 kbp threshold: dropped) with
+    long contigs at the start, around the first cut and at the end; the rows
+    must be the oracle's windows of the long contigs alone, in file order, and
+    no side file may be left."""
+    import os
+    import shutil
+    from kf2vecfsw_amd import main as M
+    rng = np.random.default_rng(4400)
+    base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else str(tmp_path)
+    work = os.path.join(base, f"kf_chunks4g_{os.getpid()}")
+    os.makedirs(os.path.join(work, "in"))
+    os.makedirs(os.path.join(work, "out"))
+    try:
+        filler = gen.wrap(gen.random_seq(rng, 9000), 80)
+        longs = [b">L%d long contig\n" % i + gen.wrap(gen.random_seq(rng, int(L)), 60)
+                 for i, L in enumerate([25000, 61000, 10000, 33333])]
+        path = os.path.join(work, "in", "big.fna")
+        pos = {}
+        with open(path, "wb") as f:
+            for i in range(480000):
+                j = 0 if i == 0 else 3 if i == 475000 else 1 if 1 not in pos and f.tell() > (1 << 30) - 40000 else None
+                for j in ([] if j is None else [j, 2] if j == 1 else [j]):
+                    pos[j] = f.tell()
+                    f.write(longs[j])
+                f.write(b">s%d\n" % i)
+                f.write(filler)
+        size = os.path.getsize(path)
+        assert size > (1 << 32)
+        cuts = [a for a, _ in M.record_pieces(path)]
+        assert len(cuts) == 5 and cuts[1] == pos[2] and pos[1] < (1 << 30) < pos[2]   # L1 | L2 at the first cut
+        M.main(["get_chunks", "-input_dir", os.path.join(work, "in"), "-output_dir", os.path.join(work, "out"),
+                "-k", "7"])
+        wins = oracle.chunk_windows(b"".join(longs), "big")
+        exp = "".join(oracle.kf_line(n, oracle.count(b">w\n" + w + b"\n", 7)[0], raw_cnt=True) for n, w in wins)
+        assert sorted(os.listdir(os.path.join(work, "out"))) == ["big.kf", "get_chunks_in.log"]
+        with open(os.path.join(work, "out", "big.kf")) as f:
+            assert f.read() == exp
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
 def test_features_handoff_equals_kf_text_round_trip(torch_dev, toy, tmp_path):
     """counter.features on the device count matrix == the float64
     values the `.kf` text holds (pd.read_csv(..., float_precision="round_trip"),

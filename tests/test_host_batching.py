@@ -119,3 +119,43 @@ def test_fasta_pieces_count_every_window_once(tmp_path, oracle, k):
                     for x, y in zip(kk.tolist(), cc.tolist()):
                         acc[x] = acc.get(x, 0) + y
                 assert sorted(acc) == ek.tolist() and [acc[x] for x in ek.tolist()] == ec.tolist(), (t, piece)
+
+
+def test_record_pieces_cut_at_headers(tmp_path, oracle):
+    """get_chunks' parts of a large FASTA file (main.record_pieces, here with tiny
+    parts): the parts tile the file, every part after the first starts at a
+    header line, a record longer than a part stays whole, a '>' inside a line is
+    no cut, and the oracle's get_chunks windows of the parts, concatenated in
+    order, are the whole file's (kf2vec/main.py:726-838: windows never span a
+    record)."""
+    import gen
+    rng = np.random.default_rng(77)
+    recs = []
+    for c in range(9):
+        L = int(rng.choice([500, 9999, 10000, 23000, 61000]))
+        seq = gen.random_seq(rng, L, lower=0.02)
+        recs.append(b">ctg%d desc>x\n" % c + gen.wrap(seq, int(rng.choice([60, 80, 0])), crlf=c == 3))
+    blob = b"text before any header\n" + b"".join(recs)
+    p = tmp_path / "g.fna"
+    p.write_bytes(blob)
+    whole = oracle.chunk_windows(blob, "s")
+    assert len(whole) > 10
+    for piece in (1, 5000, 30000, 100000, len(blob)):
+        parts = M.record_pieces(str(p), piece)
+        assert parts[0][0] == 0 and parts[-1][1] == len(blob), piece
+        assert all(parts[i][1] == parts[i + 1][0] and parts[i][0] < parts[i][1] for i in range(len(parts) - 1))
+        for a, _ in parts[1:]:
+            assert blob[a: a + 1] == b">" and blob[a - 1: a] == b"\n", (piece, a)
+        for a, e in parts[:-1]:   # cut at the first header at or after a + piece
+            assert e >= a + piece and b"\n>" not in blob[a + piece - 1: e - 1], (piece, a)
+        if piece == 1:
+            assert len(parts) == len(recs) + 1
+        if piece >= len(blob):
+            assert parts == [(0, len(blob))]
+        got = []
+        for a, e in parts:
+            got += oracle.chunk_windows(blob[a:e], "s")
+        assert got == whole, piece
+    q = tmp_path / "nohdr.fna"
+    q.write_bytes(b"ACGT" * 1000)
+    assert M.record_pieces(str(q), 10) == [(0, 4000)]

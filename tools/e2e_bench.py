@@ -77,10 +77,11 @@ def main():
     gen_s = time.perf_counter() - t0
 
     cli = ["get_frequencies", "-input_dir", inp, "-output_dir", out, "-k", str(args.k), "-p", str(args.threads)]
-    M.main(cli)                       # warm: runtime init, kernel load, page cache
-    # A/B in one process: each read mode pipelined (auto batch size), and one batch
     import contextlib
     import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        M.main(cli)                   # warm: runtime init, kernel load, page cache
+    # A/B in one process: each read mode pipelined (auto batch size), and one batch
     variants = {}
     for spec in [m for m in args.modes.split(",") if m]:
         name, _, envs = spec.partition(":")
