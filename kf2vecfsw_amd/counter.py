@@ -130,7 +130,8 @@ def pack_genomes(blobs: Sequence[bytes | np.ndarray], names: Sequence[str] | Non
 
 def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: int = N.KF_FMT_AUTO,
                pin: bool = True, threads: int = 8, pool=None, times: dict | None = None,
-               buf: torch.Tensor | None = None, index: bool = True, piece: int = 1 << 20) -> HostBatch:
+               buf: torch.Tensor | None = None, index: bool = True, piece: int = 1 << 20,
+               dev: torch.Tensor | None = None, stream=None, group: int = 16 << 20) -> HostBatch:
     """Read files straight into one (pinned) buffer and index their records.  The
     bytes come from one native call (kf_read_files: pieces of at most `piece`
     bytes read by pread on native threads, as many as `pool` has workers or
@@ -140,7 +141,12 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
     into instead of a fresh allocation (the caller makes sure no copy still reads it).
     index=False: a batch of FASTA files is not indexed here (excl None: to_device
     finds the header lines on the device, kf_index_fasta); a batch with a FASTQ
-    file is indexed on the host all the same."""
+    file is indexed on the host all the same.
+    dev (uint8 device tensor of at least the batch's bytes, pinned `buf`) and
+    stream (a torch stream): the bytes also go to dev while they are read, in
+    ranges of `group` bytes (kf_read_files_h2d); the copies are issued on stream
+    when this returns, and the batch's dev_data is dev (the caller records the
+    event that marks them done)."""
     from concurrent.futures import ThreadPoolExecutor
     import time
     t0 = time.perf_counter()
@@ -159,8 +165,15 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
         enc = [os.fsencode(p) for p in paths]
         arr = (ctypes.c_char_p * len(enc))(*enc)
         sz = np.asarray(sizes, dtype=np.uint64)
-        N.check(N.lib().kf_read_files(arr, len(enc), sz.ctypes.data, off.ctypes.data, d.ctypes.data,
-                                      int(piece), int(nthr)), "kf_read_files")
+        if dev is not None:
+            if not data.is_pinned() or dev.numel() < int(off[-1]) or dev.dtype != torch.uint8 or not dev.is_cuda:
+                raise ValueError("pack_files(dev=...): a pinned buffer and a uint8 device tensor of the batch's bytes")
+            N.check(N.lib().kf_read_files_h2d(arr, len(enc), sz.ctypes.data, off.ctypes.data, d.ctypes.data,
+                                              dev.data_ptr(), int(piece), int(nthr), int(group),
+                                              stream.cuda_stream), "kf_read_files_h2d")
+        else:
+            N.check(N.lib().kf_read_files(arr, len(enc), sz.ctypes.data, off.ctypes.data, d.ctypes.data,
+                                          int(piece), int(nthr)), "kf_read_files")
 
     def on_host(i: int) -> bool:   # FASTQ (or index=True): the host index
         return index or fmt == N.KF_FMT_FASTQ or (fmt == N.KF_FMT_AUTO and sizes[i] > 0 and d[int(off[i])] == ord("@"))
@@ -169,8 +182,14 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
         lo, sz = int(off[i]), sizes[i]
         return index_records(d[lo: lo + sz], fmt, lo)[0] if on_host(i) else None
 
+    def batch(excl):
+        hb = HostBatch(data, off, excl, list(names) if names else list(paths))
+        if dev is not None:
+            hb.dev_data = dev[: max(int(off[-1]), ALIGN)]
+        return hb
+
     if not any(on_host(i) for i in range(len(paths))):   # FASTA only: the device indexes it
-        return HostBatch(data, off, None, list(names) if names else list(paths))
+        return batch(None)
     if pool is not None:
         excl = list(pool.map(host_index, range(len(paths))))
     elif threads > 1 and len(paths) > 1:
@@ -179,11 +198,11 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
     else:
         excl = [host_index(i) for i in range(len(paths))]
     if not index and all(e is None for e in excl):
-        return HostBatch(data, off, None, list(names) if names else list(paths))
+        return batch(None)
     excl = [e if e is not None else index_records(d[int(off[i]): int(off[i]) + sizes[i]], N.KF_FMT_FASTA,
                                                   int(off[i]))[0] for i, e in enumerate(excl)]
     ex = np.concatenate(excl) if excl else np.zeros(0, np.uint64)
-    return HostBatch(data, off, ex.astype(np.uint64), list(names) if names else list(paths))
+    return batch(ex.astype(np.uint64))
 
 
 def pack_ranges(ranges: Sequence[tuple[str, int, int]], names: Sequence[str] | None = None, pin: bool = True,

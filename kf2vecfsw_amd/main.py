@@ -344,13 +344,21 @@ def get_frequencies(args) -> None:
         if slot_ev[j] is not None:
             slot_ev[j].synchronize()
         # FASTA batches are indexed on the device (to_device -> kf_index_fasta):
-        # the readers only copy the files
+        # the readers only copy the files.  The bytes go to the device on the copy
+        # stream while the batch is still being read (kf_read_files_h2d: one copy
+        # per `group` bytes read in file order), so the copy engine starts after
+        # the first 16 MiB instead of after the batch, and the H2D overlaps the
+        # reads as well as the previous batch's index, count and copy-back
+        nbytes = sum((os.path.getsize(paths[i]) + 15) // 16 * 16 for i in idx)
+        dbuf = None
+        if h2d_group:
+            with torch.cuda.stream(copy_stream):   # (the copy stream's pool: see the warm-up below)
+                dbuf = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
         hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool, times=tm,
-                        buf=slots[j], index=False)
-        # the batch goes to the device on the copy stream as soon as it is read,
-        # so its H2D overlaps the previous batch's index, count and copy-back
+                        buf=slots[j], index=False, dev=dbuf, stream=copy_stream, group=h2d_group)
         with torch.cuda.stream(copy_stream):
-            hb.dev_data = hb.data.to(device, non_blocking=True)
+            if dbuf is None:   # KF_H2D_GROUP_MB=0: one copy after the whole batch is read (round 5)
+                hb.dev_data = hb.data.to(device, non_blocking=True)
             hb.dev_event = torch.cuda.Event()
             hb.dev_event.record(copy_stream)
         slot_ev[j] = hb.dev_event   # the slot is free again once this copy has run
@@ -359,10 +367,10 @@ def get_frequencies(args) -> None:
         return hb
 
     # Three-stage pipeline over batches:
-    #   readers (2)   : read the next batches into pinned memory (one shared pool
-    #                   of host-thread file workers keeps all cores busy) and put
-    #                   each on the copy stream as soon as it is read; as many
-    #                   batches are queued for them as there are pinned slots, so
+    #   reader (1)    : reads the next batches into pinned memory (the native
+    #                   pool's threads, pieces of 1 MiB) and puts every 16 MiB
+    #                   read on the copy stream at once (kf_read_files_h2d); as many
+    #                   batches are queued for it as there are pinned slots, so
     #                   the reads (and the copies behind them) run back to back
     #                   whatever this thread is doing (r06 KF_TRACE: with only
     #                   the next two queued, the third read started when this
@@ -373,8 +381,10 @@ def get_frequencies(args) -> None:
     # The prints stay in the reference's per-file order (main.py:332-341).
     stream = torch.cuda.Stream(device)
     copy_stream = torch.cuda.Stream(device)
-    depth = int(os.environ.get("KF_READ_AHEAD", "2"))   # batches being read ahead
-    reader = ThreadPoolExecutor(max_workers=depth)
+    h2d_group = int(float(os.environ.get("KF_H2D_GROUP_MB", "16")) * (1 << 20))
+    # one reader: a batch's read already uses every host thread, and its copies
+    # then reach the copy stream in file order, ahead of the next batch's
+    reader = ThreadPoolExecutor(max_workers=int(os.environ.get("KF_READERS", "1")))
     writer = ThreadPoolExecutor(max_workers=1)
     ahead = n_slots   # batches queued for the readers (read, or copied, but not yet counted)
     reads = deque(reader.submit(pack, i, batches[i]) for i in range(min(ahead, len(batches))))
