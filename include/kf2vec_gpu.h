@@ -99,17 +99,6 @@ int kf_index_records(const uint8_t* bytes, uint64_t len, int fmt, uint64_t base,
 int kf_read_files(const char* const* paths, int32_t n, const uint64_t* sizes, const uint64_t* off,
                   uint8_t* dst, uint64_t piece, int n_threads);
 
-/* kf_read_files into a pinned host buffer `dst` that also copies the bytes to
- * the device buffer d_dst (same offsets) while it reads: whenever the bytes
- * read so far in file order, from off[0], are `group` bytes (or the rest) past
- * the last copy, that range goes out as one hipMemcpyAsync on `stream`, so the
- * copy engine starts after the first group instead of after the batch.  On
- * return every copy is issued (not done): the caller records an event on
- * `stream` before it reuses dst. */
-int kf_read_files_h2d(const char* const* paths, int32_t n, const uint64_t* sizes, const uint64_t* off,
-                      uint8_t* dst, uint8_t* d_dst, uint64_t piece, int n_threads, uint64_t group,
-                      void* stream);
-
 /* The FASTA record index of a batch resident in HBM (what kf_index_records finds
  * per file, found on the device so the host only copies the files): the header
  * lines -- a line starting with '>' at a genome start or after '\n', up to its

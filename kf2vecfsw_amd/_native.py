@@ -57,7 +57,6 @@ SIGNATURES = {
     "kf_chunk_gather": (_int, [_vp, _vp, _i32, _u32, _vp, _vp]),
     "kf_index_fasta": (_int, [_vp, _vp, _i32, _u64, _vp, _u64, _vp, _vp, _u64, _vp]),
     "kf_read_files": (_int, [ctypes.POINTER(_cp), _i32, _vp, _vp, _vp, _u64, _int]),
-    "kf_read_files_h2d": (_int, [ctypes.POINTER(_cp), _i32, _vp, _vp, _vp, _vp, _u64, _int, _u64, _vp]),
     "kf_sparse_workspace_bytes": (_u64, [_int, _u64, _i32]),
     "kf_sparse_count": (_int, [_vp, _vp, _i32, _u64, _vp, _u64, _int, _vp, _u64, _vp, _vp, _vp, _vp]),
 }

@@ -130,8 +130,7 @@ def pack_genomes(blobs: Sequence[bytes | np.ndarray], names: Sequence[str] | Non
 
 def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: int = N.KF_FMT_AUTO,
                pin: bool = True, threads: int = 8, pool=None, times: dict | None = None,
-               buf: torch.Tensor | None = None, index: bool = True, piece: int = 1 << 20,
-               dev: torch.Tensor | None = None, stream=None, group: int = 16 << 20) -> HostBatch:
+               buf: torch.Tensor | None = None, index: bool = True, piece: int = 1 << 20) -> HostBatch:
     """Read files straight into one (pinned) buffer and index their records.  The
     bytes come from one native call (kf_read_files: pieces of at most `piece`
     bytes read by pread on native threads, as many as `pool` has workers or
@@ -141,12 +140,7 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
     into instead of a fresh allocation (the caller makes sure no copy still reads it).
     index=False: a batch of FASTA files is not indexed here (excl None: to_device
     finds the header lines on the device, kf_index_fasta); a batch with a FASTQ
-    file is indexed on the host all the same.
-    dev (uint8 device tensor of at least the batch's bytes, pinned `buf`) and
-    stream (a torch stream): the bytes also go to dev while they are read, in
-    ranges of `group` bytes (kf_read_files_h2d); the copies are issued on stream
-    when this returns, and the batch's dev_data is dev (the caller records the
-    event that marks them done)."""
+    file is indexed on the host all the same."""
     from concurrent.futures import ThreadPoolExecutor
     import time
     t0 = time.perf_counter()
@@ -165,15 +159,8 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
         enc = [os.fsencode(p) for p in paths]
         arr = (ctypes.c_char_p * len(enc))(*enc)
         sz = np.asarray(sizes, dtype=np.uint64)
-        if dev is not None:
-            if not data.is_pinned() or dev.numel() < int(off[-1]) or dev.dtype != torch.uint8 or not dev.is_cuda:
-                raise ValueError("pack_files(dev=...): a pinned buffer and a uint8 device tensor of the batch's bytes")
-            N.check(N.lib().kf_read_files_h2d(arr, len(enc), sz.ctypes.data, off.ctypes.data, d.ctypes.data,
-                                              dev.data_ptr(), int(piece), int(nthr), int(group),
-                                              stream.cuda_stream), "kf_read_files_h2d")
-        else:
-            N.check(N.lib().kf_read_files(arr, len(enc), sz.ctypes.data, off.ctypes.data, d.ctypes.data,
-                                          int(piece), int(nthr)), "kf_read_files")
+        N.check(N.lib().kf_read_files(arr, len(enc), sz.ctypes.data, off.ctypes.data, d.ctypes.data,
+                                      int(piece), int(nthr)), "kf_read_files")
 
     def on_host(i: int) -> bool:   # FASTQ (or index=True): the host index
         return index or fmt == N.KF_FMT_FASTQ or (fmt == N.KF_FMT_AUTO and sizes[i] > 0 and d[int(off[i])] == ord("@"))
@@ -183,10 +170,7 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
         return index_records(d[lo: lo + sz], fmt, lo)[0] if on_host(i) else None
 
     def batch(excl):
-        hb = HostBatch(data, off, excl, list(names) if names else list(paths))
-        if dev is not None:
-            hb.dev_data = dev[: max(int(off[-1]), ALIGN)]
-        return hb
+        return HostBatch(data, off, excl, list(names) if names else list(paths))
 
     if not any(on_host(i) for i in range(len(paths))):   # FASTA only: the device indexes it
         return batch(None)
@@ -320,6 +304,9 @@ def _stream_ptr(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_DEV_TABLES: dict = {}   # (k, device index) -> (code2col, col2rep) on the device
+
+
 class KmerCounter:
     """Canonical k-mer counter for one k on one device (the ``jellyfish count -C
     -m k`` + ``dump -c`` + vocab merge of main.py:309-328)."""
@@ -332,9 +319,12 @@ class KmerCounter:
         if self.device.type != "cuda" or not torch.cuda.is_available():
             raise N.NativeError("KmerCounter needs a ROCm GPU (no CPU fallback)")
         self.nbins = num_bins(k)
-        c2c, c2r = tables(k)
-        self.code2col = torch.from_numpy(c2c.view(np.int32)).to(self.device)
-        self.col2rep = torch.from_numpy(c2r.view(np.int32)).to(self.device)
+        key = (k, self.device.index if self.device.index is not None else torch.cuda.current_device())
+        if key not in _DEV_TABLES:   # immutable: one upload per (k, device) and process
+            c2c, c2r = tables(k)
+            _DEV_TABLES[key] = (torch.from_numpy(c2c.view(np.int32)).to(self.device),
+                                torch.from_numpy(c2r.view(np.int32)).to(self.device))
+        self.code2col, self.col2rep = _DEV_TABLES[key]
 
     def launch_info(self) -> tuple[int, int, int]:
         g, b, l = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

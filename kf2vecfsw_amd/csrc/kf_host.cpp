@@ -511,14 +511,8 @@ static void host_parallel(uint64_t n, int n_threads, const std::function<void(ui
         }
 }
 
-// kf_read_files with a progress callback: ready(lo, hi, ctx) is called for
-// consecutive ranges [lo, hi) of dst, from off[0] to off[n], as soon as every
-// byte in them (file bytes and padding) is in place: in order, one call at a
-// time, each at least `group` bytes but the last (kf_read_files_h2d copies each
-// range to the device while the later pieces are still being read).
-int kf_read_files_cb(const char* const* paths, int32_t n, const uint64_t* sizes, const uint64_t* off,
-                     uint8_t* dst, uint64_t piece, int n_threads, uint64_t group,
-                     int (*ready)(uint64_t lo, uint64_t hi, void* ctx), void* ctx) {
+extern "C" int kf_read_files(const char* const* paths, int32_t n, const uint64_t* sizes, const uint64_t* off,
+                             uint8_t* dst, uint64_t piece, int n_threads) {
     if (n < 0 || (n && (!paths || !sizes || !off || !dst))) return kf_fail(KF_EINVAL, "null argument");
     if (n == 0) return KF_OK;
     if (piece < 4096) piece = 4096;
@@ -545,24 +539,6 @@ int kf_read_files_cb(const char* const* paths, int32_t n, const uint64_t* sizes,
             break;
         }
     }
-    for (int32_t i = 0; i < n; ++i)   // empty files: their padding (no piece covers them)
-        if (sizes[i] == 0) memset(dst + off[i], '\n', off[i + 1] - off[i]);
-    // progress: pieces in byte order; `front` = the first piece not yet done
-    std::vector<uint8_t> done(ready ? npiece : 0, 0);
-    uint64_t front = 0, issued = off[0];
-    auto piece_start = [&](uint64_t t) {   // dst offset of piece t (t < npiece)
-        const int32_t i = (int32_t)(std::upper_bound(first.begin(), first.end(), t) - first.begin()) - 1;
-        return off[i] + (t - first[i]) * piece;
-    };
-    auto advance = [&](uint64_t t) {   // caller holds mu
-        done[t] = 1;
-        while (front < npiece && done[front]) ++front;
-        const uint64_t hi = front == npiece ? off[n] : piece_start(front);
-        if (hi > issued && (hi - issued >= group || front == npiece)) {
-            if (!err.load() && ready(issued, hi, ctx) != 0 && !err.exchange(1)) errmsg = "the ready callback failed";
-            issued = hi;
-        }
-    };
     auto piece_fn = [&](uint64_t t) {
         {
             if (err.load()) return;
@@ -579,24 +555,15 @@ int kf_read_files_cb(const char* const* paths, int32_t n, const uint64_t* sizes,
                 got += (uint64_t)r;
             }
             if (e == sizes[i]) memset(dst + off[i] + sizes[i], '\n', off[i + 1] - off[i] - sizes[i]);
-            if (ready) {
-                std::lock_guard<std::mutex> lk(mu);
-                advance(t);
-            }
         }
     };
     if (!err.load()) host_parallel(npiece, n_threads, piece_fn);
     for (int32_t i = 0; i < n; ++i)
         if (fds[i] >= 0) close(fds[i]);
-    if (!err.load() && ready && issued < off[n] && ready(issued, off[n], ctx) != 0)   // (no pieces: empty files only)
-        fail("the ready callback failed");
+    for (int32_t i = 0; i < n; ++i)   // empty files: their padding (no piece covers them)
+        if (sizes[i] == 0) memset(dst + off[i], '\n', off[i + 1] - off[i]);
     if (err.load()) return kf_fail(KF_EINVAL, "%s", errmsg.c_str());
     return KF_OK;
-}
-
-extern "C" int kf_read_files(const char* const* paths, int32_t n, const uint64_t* sizes, const uint64_t* off,
-                             uint8_t* dst, uint64_t piece, int n_threads) {
-    return kf_read_files_cb(paths, n, sizes, off, dst, piece, n_threads, 0, nullptr, nullptr);
 }
 
 extern "C" int kf_format_kf(const char* name, const uint32_t* counts, uint64_t nbins, int pseudocount,

@@ -153,26 +153,3 @@ extern "C" int kf_index_fasta(const uint8_t* d_bytes, const uint64_t* d_goff, in
     if (hipGetLastError() != hipSuccess) return kf_fail(KF_EHIP, "record index launch failed");
     return KF_OK;
 }
-
-// ---- the CLI's read + copy: file bytes go to the device while later pieces of
-// the same batch are still being read (kf_read_files_cb's ranges, each one
-// hipMemcpyAsync from the pinned buffer on `stream`).
-namespace {
-struct H2dCtx {
-    const uint8_t* host;
-    uint8_t* dev;
-    hipStream_t stream;
-};
-int h2d_ready(uint64_t lo, uint64_t hi, void* p) {
-    const H2dCtx& c = *(const H2dCtx*)p;
-    return hipMemcpyAsync(c.dev + lo, c.host + lo, hi - lo, hipMemcpyHostToDevice, c.stream) == hipSuccess ? 0 : 1;
-}
-}  // namespace
-
-extern "C" int kf_read_files_h2d(const char* const* paths, int32_t n, const uint64_t* sizes, const uint64_t* off,
-                                 uint8_t* dst, uint8_t* d_dst, uint64_t piece, int n_threads, uint64_t group,
-                                 void* stream) {
-    if (n && !d_dst) return kf_fail(KF_EINVAL, "null argument");
-    H2dCtx c{dst, d_dst, (hipStream_t)stream};
-    return kf_read_files_cb(paths, n, sizes, off, dst, piece, n_threads, group < 4096 ? 4096 : group, &h2d_ready, &c);
-}

@@ -12,7 +12,6 @@ from __future__ import annotations
 
 import argparse
 import ctypes
-import fnmatch
 import multiprocessing as mp
 import os
 import sys
@@ -30,12 +29,13 @@ max_k_len = 31             # main.py:82
 supported_k = range(3, 12)  # rule-generated vocab (reference ships 3..9; 10 is a missing blob)
 
 FORMATS = [".fq", ".fastq", ".fa", ".fna", ".fasta"]   # main.py:272
+_SUFFIXES = tuple(FORMATS)
 
 
 def list_inputs(input_dir: str) -> tuple[list[str], list[str]]:
     """main.py:272-275: files in os.listdir order and their sample names."""
-    files_names = [f for f in os.listdir(input_dir)
-                   if True in (fnmatch.fnmatch(f, "*" + form) for form in FORMATS)]
+    # (fnmatch "*" + form on POSIX is a case-sensitive suffix test)
+    files_names = [f for f in os.listdir(input_dir) if f.endswith(_SUFFIXES)]
     samples_names = [f.rsplit(".f", 1)[0] for f in files_names]
     return files_names, samples_names
 
@@ -63,7 +63,7 @@ def format_kf(name: str, counts: np.ndarray, pseudocount: bool = False, raw_cnt:
     return buf.raw[: w.value]
 
 
-def _pipeline_budget(paths: list[str], batch_gb) -> int:
+def _pipeline_budget(paths: list[str], batch_gb, sizes: list[int] | None = None) -> int:
     """Bytes per batch: -batch_gb if given, else about a quarter of the input
     (so reading, copying, counting and writing overlap; 64 x 5 Mbp on two boxes,
     tools/e2e_bench.py: 4 parts 26.1 and 32.9 Gbases/s against 8 parts 22.5 and
@@ -71,7 +71,7 @@ def _pipeline_budget(paths: list[str], batch_gb) -> int:
     [16 MiB, 4 GiB].  KF_BATCH_PARTS overrides the part count."""
     if batch_gb:
         return int(float(batch_gb) * (1 << 30))
-    total = sum(os.path.getsize(p) for p in paths)
+    total = sum(sizes) if sizes is not None else sum(os.path.getsize(p) for p in paths)
     parts = int(os.environ.get("KF_BATCH_PARTS", "4"))
     return int(min(max(total // parts, 16 << 20), 4 << 30))
 
@@ -241,6 +241,8 @@ def cli_host_threads(args) -> int:
 def get_frequencies(args) -> None:
     """kf2vec/main.py:250-373 on the GPU (-gpus N: byte-balanced file shards, one
     process per GPU)."""
+    import time
+    t_entry = time.perf_counter()
     shard = _shard_spec(args)
     lead = shard is None or shard[0] == 0
     if getattr(args, "gpus", 1) != 1 and int(os.environ.get("WORLD_SIZE", "1")) > 1 and not os.environ.get("KF_SHARD"):
@@ -309,8 +311,10 @@ def get_frequencies(args) -> None:
     # ... and at most _count_cap genomes, so the count matrix of a batch (on the
     # device, pinned for the writer, `behind` batches deep) stays bounded at any k
     batch_gb = getattr(args, "batch_gb", None)
-    batches = _batches(paths, _pipeline_budget(paths, batch_gb), ramp=True,
-                       max_files=_count_cap(4 * counter.nbins, batch_gb))
+    fsz = [os.path.getsize(p) for p in paths]
+    asz = [(x + 15) // 16 * 16 for x in fsz]   # bytes in a batch (16-byte aligned files)
+    batches = _size_batches(fsz, _pipeline_budget(paths, batch_gb, fsz), ramp=True,
+                            max_files=_count_cap(4 * counter.nbins, batch_gb))
     # the reference processes files in order and later ones overwrite earlier
     # ones with the same sample name: keep the last occurrence only
     last = {s: i for i, s in enumerate(samples_names)}
@@ -322,7 +326,6 @@ def get_frequencies(args) -> None:
     # KF_TRACE=1: per-batch stage timeline on stderr (host ms; device events ms
     # from the first H2D's start event), for tools/e2e_bench.py
     trace = os.environ.get("KF_TRACE") == "1"
-    import time
     t_origin = time.perf_counter()
     tr: list = []
 
@@ -332,7 +335,7 @@ def get_frequencies(args) -> None:
     # pinned input slots, reused round robin (a fresh pinned block per batch costs
     # ~1 ms of allocation on the reader's path): batch i reads into slot i mod
     # n_slots once the H2D that last read that slot has completed
-    slot_bytes = max(sum((os.path.getsize(paths[i]) + 15) // 16 * 16 for i in b) for b in batches)
+    slot_bytes = max(sum(asz[i] for i in b) for b in batches)
     n_slots = min(len(batches), int(os.environ.get("KF_READ_AHEAD", "2")) + 2)
     slots = [torch.empty(max(slot_bytes, 16), dtype=torch.uint8, pin_memory=True) for _ in range(n_slots)]
     slot_ev: list = [None] * n_slots
@@ -344,21 +347,15 @@ def get_frequencies(args) -> None:
         if slot_ev[j] is not None:
             slot_ev[j].synchronize()
         # FASTA batches are indexed on the device (to_device -> kf_index_fasta):
-        # the readers only copy the files.  The bytes go to the device on the copy
-        # stream while the batch is still being read (kf_read_files_h2d: one copy
-        # per `group` bytes read in file order), so the copy engine starts after
-        # the first 16 MiB instead of after the batch, and the H2D overlaps the
-        # reads as well as the previous batch's index, count and copy-back
-        nbytes = sum((os.path.getsize(paths[i]) + 15) // 16 * 16 for i in idx)
-        dbuf = None
-        if h2d_group:
-            with torch.cuda.stream(copy_stream):   # (the copy stream's pool: see the warm-up below)
-                dbuf = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+        # the readers only copy the files
         hb = pack_files([paths[i] for i in idx], [samples_names[i] for i in idx], pool=files_pool, times=tm,
-                        buf=slots[j], index=False, dev=dbuf, stream=copy_stream, group=h2d_group)
+                        buf=slots[j], index=False)
+        # the batch goes to the device on the copy stream as soon as it is read,
+        # so its H2D overlaps the previous batch's index, count and copy-back
+        # (copies issued while the batch is read, 16 MiB at a time from the
+        # native readers, measured no faster: DESIGN section 8)
         with torch.cuda.stream(copy_stream):
-            if dbuf is None:   # KF_H2D_GROUP_MB=0: one copy after the whole batch is read (round 5)
-                hb.dev_data = hb.data.to(device, non_blocking=True)
+            hb.dev_data = hb.data.to(device, non_blocking=True)
             hb.dev_event = torch.cuda.Event()
             hb.dev_event.record(copy_stream)
         slot_ev[j] = hb.dev_event   # the slot is free again once this copy has run
@@ -367,10 +364,10 @@ def get_frequencies(args) -> None:
         return hb
 
     # Three-stage pipeline over batches:
-    #   reader (1)    : reads the next batches into pinned memory (the native
-    #                   pool's threads, pieces of 1 MiB) and puts every 16 MiB
-    #                   read on the copy stream at once (kf_read_files_h2d); as many
-    #                   batches are queued for it as there are pinned slots, so
+    #   readers (2)   : read the next batches into pinned memory (the native
+    #                   pool's threads, pieces of 1 MiB) and put each on the copy
+    #                   stream as soon as it is read; as many
+    #                   batches are queued for them as there are pinned slots, so
     #                   the reads (and the copies behind them) run back to back
     #                   whatever this thread is doing (r06 KF_TRACE: with only
     #                   the next two queued, the third read started when this
@@ -381,10 +378,10 @@ def get_frequencies(args) -> None:
     # The prints stay in the reference's per-file order (main.py:332-341).
     stream = torch.cuda.Stream(device)
     copy_stream = torch.cuda.Stream(device)
-    h2d_group = int(float(os.environ.get("KF_H2D_GROUP_MB", "16")) * (1 << 20))
-    # one reader: a batch's read already uses every host thread, and its copies
-    # then reach the copy stream in file order, ahead of the next batch's
-    reader = ThreadPoolExecutor(max_workers=int(os.environ.get("KF_READERS", "1")))
+    # two readers: one read call's tail (its last pieces, the files' opens) and
+    # the writer's formatting leave host threads idle that a second batch's read
+    # fills
+    reader = ThreadPoolExecutor(max_workers=int(os.environ.get("KF_READERS", "2")))
     writer = ThreadPoolExecutor(max_workers=1)
     ahead = n_slots   # batches queued for the readers (read, or copied, but not yet counted)
     reads = deque(reader.submit(pack, i, batches[i]) for i in range(min(ahead, len(batches))))
@@ -392,7 +389,7 @@ def get_frequencies(args) -> None:
     # and the device block for a batch (the caching allocator keeps it for this
     # stream) would otherwise cost ~2 ms between the first read and its H2D
     # (KF_TRACE: got 0 -> issue 0, tools/e2e_bench.py).
-    big = max(sum((os.path.getsize(paths[i]) + 15) // 16 * 16 for i in b) for b in batches)
+    big = slot_bytes
     with torch.cuda.stream(copy_stream):   # the batches' device blocks come from the copy stream's pool
         warm = torch.empty(big + 16, dtype=torch.uint8, device=device)
         warm[:16].zero_()
@@ -461,6 +458,7 @@ def get_frequencies(args) -> None:
             tr.append(("issue", bi, th))   # after: to_device, count, pinned alloc, D2H, prints+submit
     for w in writes:
         w.result()
+    t_written = now_ms()
     reader.shutdown()
     writer.shutdown()
     files_pool.shutdown()
@@ -471,7 +469,8 @@ def get_frequencies(args) -> None:
             d = [round(base_cpu + e00.elapsed_time(x), 3) for x in e]
             tr.append(("gpu", bi, t_issue, {"h2d": d[:2], "count": d[1:3], "d2h": d[2:4]}))
         import json
-        print(json.dumps({"kf_trace": tr, "total_ms": now_ms()}), file=sys.stderr)
+        print(json.dumps({"kf_trace": tr, "total_ms": now_ms(), "written_ms": t_written,
+                          "setup_ms": round((t_origin - t_entry) * 1e3, 3)}), file=sys.stderr)
 
     _finish(args, shard, lead)
 
@@ -1089,8 +1088,21 @@ def build_parser() -> argparse.ArgumentParser:
     return parser
 
 
+_PARSER: list = []   # (mp.cpu_count() it was built for, parser)
+
+
+def _parser() -> argparse.ArgumentParser:
+    """build_parser(), kept for later calls in the process (a library caller that
+    runs the CLI per directory; building it costs ~1-3 ms), rebuilt if the CPU
+    count its -p choices were made for has changed."""
+    n = mp.cpu_count()
+    if not _PARSER or _PARSER[0][0] != n:
+        _PARSER[:] = [(n, build_parser())]
+    return _PARSER[0][1]
+
+
 def main(argv=None) -> None:
-    parser = build_parser()
+    parser = _parser()
     args = parser.parse_args(argv)
     if os.environ.get("KF_SHARD"):
         # a -gpus child shares its parent's stdout with the other shards: one

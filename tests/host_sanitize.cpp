@@ -12,8 +12,7 @@
 //     reports the pair count the full call then returns;
 //   * kf_format_kf: every field parses back (strtod) to count/sum, count+0.5 or
 //     the integer count, as main.py:327-345 defines them; written <= capacity;
-//   * kf_write_kf_files (8 threads): each file equals kf_format_kf's line;
-//   * kf_read_files_cb: in-order, complete ranges (the CLI's read + copy).
+//   * kf_write_kf_files (8 threads): each file equals kf_format_kf's line.
 #include <dirent.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -27,7 +26,6 @@
 #include <vector>
 
 #include "../include/kf2vec_gpu.h"
-#include "../kf2vecfsw_amd/csrc/kf_internal.h"
 
 static int g_fail = 0;
 #define CHECK(c)                                                                        \
@@ -190,64 +188,6 @@ static void writer(std::mt19937_64& rng) {
     rmdir(dir);
 }
 
-// kf_read_files_cb (the CLI's read + copy, kf_read_files_h2d without the copy):
-// the ranges it hands out are consecutive from off[0] to off[n], each >= group
-// bytes but the last, and every byte of a range is final when it is handed out
-// (file bytes, '\n' padding, empty files); several piece sizes and thread counts.
-struct CbState {
-    const uint8_t* dst;
-    const std::vector<uint8_t>* expect;
-    uint64_t next, group, end;
-    int calls, bad;
-};
-static int cb_check(uint64_t lo, uint64_t hi, void* p) {
-    CbState& s = *(CbState*)p;
-    ++s.calls;
-    if (lo != s.next || hi <= lo || (hi - lo < s.group && hi != s.end) ||
-        memcmp(s.dst + lo, s.expect->data() + lo, hi - lo) != 0)
-        ++s.bad;
-    s.next = hi;
-    return 0;
-}
-static void read_files_cb(std::mt19937_64& rng) {
-    char tmpl[] = "/tmp/kf_host_sanitize_rd_XXXXXX";
-    const char* dir = mkdtemp(tmpl);
-    CHECK(dir != nullptr);
-    if (!dir) return;
-    const int n = 9;
-    std::vector<std::string> nm(n);
-    std::vector<const char*> paths(n);
-    std::vector<uint64_t> sizes(n), off(n + 1, 0);
-    std::vector<uint8_t> expect;
-    for (int i = 0; i < n; ++i) {
-        sizes[i] = i == 3 ? 0 : (uint64_t)(rng() % 300000);
-        nm[i] = std::string(dir) + "/f" + std::to_string(i);
-        paths[i] = nm[i].c_str();
-        std::vector<uint8_t> b(sizes[i]);
-        for (auto& x : b) x = (uint8_t)("ACGT>\nN"[rng() % 7]);
-        FILE* f = fopen(paths[i], "wb");
-        CHECK(f != nullptr);
-        if (!f) return;
-        if (!b.empty()) fwrite(b.data(), 1, b.size(), f);
-        fclose(f);
-        off[i + 1] = off[i] + (sizes[i] + 15) / 16 * 16;
-        b.resize(off[i + 1] - off[i], '\n');
-        expect.insert(expect.end(), b.begin(), b.end());
-    }
-    for (uint64_t piece : {4096ull, 65536ull, 1ull << 20})
-        for (int thr : {1, 3, 8})
-            for (uint64_t group : {1ull, 50000ull, 1ull << 30}) {
-                std::vector<uint8_t> dst(off[n], 0xAB);
-                CbState st{dst.data(), &expect, 0, group, off[n], 0, 0};
-                CHECK(kf_read_files_cb(paths.data(), n, sizes.data(), off.data(), dst.data(), piece, thr, group,
-                                       &cb_check, &st) == KF_OK);
-                CHECK(st.bad == 0 && st.next == off[n] && st.calls >= 1);
-                CHECK(memcmp(dst.data(), expect.data(), off[n]) == 0);
-            }
-    for (int i = 0; i < n; ++i) unlink(paths[i]);
-    rmdir(dir);
-}
-
 int main() {
     std::mt19937_64 rng(20260101);
     CHECK(kf_abi_version() == 1);
@@ -255,7 +195,6 @@ int main() {
     index_records(rng);
     format(rng);
     writer(rng);
-    read_files_cb(rng);
     for (int64_t g : {0, 7, 12345, -3}) {
         CHECK(kf_synth_header_len(g) >= 7);
         CHECK(kf_synth_genome_bytes(g, 5000, 80, 256) % 256 == 0);

@@ -91,6 +91,25 @@ def main():
         th.join()
         res["read_under_dma_GBps"].append(round(total / min(ts) / 1e9, 1))
         res["h2d_under_reads_GBps"].append(round(copied[0] / copied[1] / 1e9, 1))
+    # H2D of the whole batch in ranges of `mb` MiB, on one stream or alternating two
+    s2 = torch.cuda.Stream(dev)
+    big = torch.empty(total, dtype=torch.uint8, device=dev)
+    hsrc = buf[:total]
+    res["h2d_chunked_GBps"] = {}
+    for mb in (4, 16, 64, 320):
+        for ns in (1, 2):
+            best = 0.0
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                step = mb << 20
+                for i, a in enumerate(range(0, total, step)):
+                    st = (s, s2)[i % ns]
+                    with torch.cuda.stream(st):
+                        big[a: a + step].copy_(hsrc[a: a + step], non_blocking=True)
+                torch.cuda.synchronize()
+                best = max(best, total / (time.perf_counter() - t0) / 1e9)
+            res["h2d_chunked_GBps"][f"{mb}MiB_x{ns}"] = round(best, 1)
     print(json.dumps(res))
     shutil.rmtree(d, ignore_errors=True)
 
