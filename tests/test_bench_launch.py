@@ -83,3 +83,34 @@ def test_bench_gpus2_spawns_two_ranks():
     assert out["ranks"]["launcher"].startswith("bench.py --gpus")
     assert "BASELINE configs[3]" in out["config"]["workload"] and out["config"]["global_batch"] == 64
     assert out["parity"] == "ok"
+
+
+@pytest.mark.gpu
+def test_bench_rccl_collectives_one_rank():
+    """The RCCL side of bench.py's multi-GPU path, which the driver's 8-GPU SCALE
+    run is the first to execute with more than one GPU: init_process_group("nccl",
+    device_id=...) as bench.main calls it, then Workload's own barrier, all_ok
+    (float32 MAX) and max_over_ranks (float64 MAX) on device tensors, over a
+    one-rank RCCL group (the methods run their collectives whenever world > 1)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    code = "\n".join([
+        "import os, sys, torch, torch.distributed as dist",
+        f"sys.path.insert(0, {ROOT!r})",
+        "import bench",
+        f"os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT='{port}', RANK='0', WORLD_SIZE='1', LOCAL_RANK='0')",
+        "torch.cuda.set_device(0)",
+        "dist.init_process_group('nccl', device_id=torch.device('cuda', 0))",
+        "W = bench.Workload.__new__(bench.Workload)",
+        "W.torch, W.dev, W.world, W.dist, W.rehearse = torch, torch.device('cuda', 0), 2, dist, False",
+        "W.barrier()",
+        "assert W.all_ok(True) and not W.all_ok(False)",
+        "assert W.max_over_ranks(1.5, 2.25) == (1.5, 2.25)",
+        "assert dist.get_backend() == 'nccl'",
+        "dist.destroy_process_group()",
+        "print('rccl ok')",
+    ])
+    p = subprocess.run([sys.executable, "-c", code], env=_env(), capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "rccl ok" in p.stdout, p.stderr[-3000:]
