@@ -169,11 +169,8 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
         lo, sz = int(off[i]), sizes[i]
         return index_records(d[lo: lo + sz], fmt, lo)[0] if on_host(i) else None
 
-    def batch(excl):
-        return HostBatch(data, off, excl, list(names) if names else list(paths))
-
     if not any(on_host(i) for i in range(len(paths))):   # FASTA only: the device indexes it
-        return batch(None)
+        return HostBatch(data, off, None, list(names) if names else list(paths))
     if pool is not None:
         excl = list(pool.map(host_index, range(len(paths))))
     elif threads > 1 and len(paths) > 1:
@@ -182,11 +179,11 @@ def pack_files(paths: Sequence[str], names: Sequence[str] | None = None, fmt: in
     else:
         excl = [host_index(i) for i in range(len(paths))]
     if not index and all(e is None for e in excl):
-        return batch(None)
+        return HostBatch(data, off, None, list(names) if names else list(paths))
     excl = [e if e is not None else index_records(d[int(off[i]): int(off[i]) + sizes[i]], N.KF_FMT_FASTA,
                                                   int(off[i]))[0] for i, e in enumerate(excl)]
     ex = np.concatenate(excl) if excl else np.zeros(0, np.uint64)
-    return batch(ex.astype(np.uint64))
+    return HostBatch(data, off, ex.astype(np.uint64), list(names) if names else list(paths))
 
 
 def pack_ranges(ranges: Sequence[tuple[str, int, int]], names: Sequence[str] | None = None, pin: bool = True,
