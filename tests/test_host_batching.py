@@ -159,3 +159,17 @@ def test_record_pieces_cut_at_headers(tmp_path, oracle):
     q = tmp_path / "nohdr.fna"
     q.write_bytes(b"ACGT" * 1000)
     assert M.record_pieces(str(q), 10) == [(0, 4000)]
+
+
+def test_list_inputs_matches_reference_fnmatch(tmp_path):
+    """main.list_inputs (a suffix test) picks the same files, in the same
+    os.listdir order, as the reference's fnmatch over "*" + form
+    (kf2vec/main.py:272-275), on names around the patterns."""
+    import fnmatch
+    names = ["a.fa", "b.FA", "c.fasta.gz", ".fa", "x.fq", "y.fastq", "z.fna~", "w.fa.fa", "v.fna", "u.fasta",
+             "t.fq.txt", "sfa", "r.f", "q.fastqq", "p[1].fa", "o*.fna", "n?.fq"]
+    for n in names:
+        (tmp_path / n).write_bytes(b">x\nACGT\n")
+    exp = [f for f in os.listdir(tmp_path) if True in (fnmatch.fnmatch(f, "*" + form) for form in M.FORMATS)]
+    files, samples = M.list_inputs(str(tmp_path))
+    assert files == exp and samples == [f.rsplit(".f", 1)[0] for f in exp]
