@@ -73,14 +73,20 @@ constexpr uint32_t kNB = 1u << kBD;
 __host__ __device__ constexpr int sp_dbits(int k) { return 2 * k < kBD ? 2 * k : kBD; }
 // Phase C: chunks of at most 32 keys per thread (16,384 at 512 threads: 128 KiB
 // of LDS for u64 keys), up to 256 VGPRs per thread (1024 threads spilled at 128).
-// KF_SP_CBLOCK = 256 (tools/ A/B builds): 8,192-key chunks, two workgroups per CU.
+// tools/ A/B builds: KF_SP_CBLOCK = 256, 8,192-key chunks, two workgroups per CU;
+// KF_SP_CBLOCK = 768 with KF_SP_CPER = 16 keys per thread, 12,288-key chunks
+// and 12 waves per CU.
 #ifndef KF_SP_CBLOCK
 #define KF_SP_CBLOCK 512
 #endif
+#ifndef KF_SP_CPER
+#define KF_SP_CPER 32
+#endif
 constexpr int kCBlock = KF_SP_CBLOCK;
 constexpr int kCWaves = kCBlock / 64;
-constexpr uint32_t kCCap = 32u * (uint32_t)kCBlock;
-constexpr int kCPerCU = 512 / kCBlock;   // resident chunk workgroups per CU
+constexpr uint32_t kCCap = (uint32_t)KF_SP_CPER * (uint32_t)kCBlock;
+constexpr int kCPerCU = kCBlock >= 512 ? 1 : 512 / kCBlock;   // resident chunk workgroups per CU
+constexpr int kCWavesPerEU = (kCWaves * kCPerCU + 3) / 4;
 template <typename KeyT>
 struct ChunkOf {
     static constexpr uint32_t cap = kCCap;                          // keys
@@ -953,7 +959,7 @@ __device__ __forceinline__ uint32_t ceil_log2(uint32_t x) { return x <= 1 ? 0u :
 // soon as a chunk is sorted and first used when its sort starts, so their
 // latency hides behind the encoding.
 template <typename KeyT>
-__global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2))) sp2_chunk_kernel(const KeyT* __restrict__ kb, const KeyT* __restrict__ ovf,
+__global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kCWavesPerEU))) sp2_chunk_kernel(const KeyT* __restrict__ kb, const KeyT* __restrict__ ovf,
                                                             const Chunk* chunks, const uint32_t* cfirst, int n,
                                                             int bshift, const uint64_t* goff, uint32_t* flags,
                                                             uint64_t* cstatus, uint32_t* ticket,
@@ -963,8 +969,9 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
     using CO = ChunkOf<KeyT>;
     constexpr int PER = CO::per;
     constexpr uint32_t kWords = CO::cap / 32;   // mask words of a chunk
-    static_assert(kWords == (uint32_t)kCBlock && kCWaves * kNWW >= 2 * kWords && kNWW <= (uint32_t)kCBlock,
-                  "one mask word per thread");
+    static_assert(kWords <= (uint32_t)kCBlock && kCWaves * kNWW >= 2 * kWords && kNWW <= (uint32_t)kCBlock,
+                  "at most one mask word per thread");
+    const bool word_owner = threadIdx.x < kWords;   // (threads past kWords own no mask word)
     __shared__ uint32_t wc[kCWaves][kNWW];   // packed u16 digit counters per wave; after the sort: start | head masks
     __shared__ uint32_t wpre[kWords];       // heads before each head-mask word
     __shared__ uint32_t wsum[kCWaves];
@@ -1115,7 +1122,7 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
                 // recomputes the head bits inside it
                 bool lng = false;
                 {
-                    const uint32_t m = hs[tid], nb0 = tid + 1 < (int)kWords ? hs[tid + 1] & 1u : 0u;
+                    const uint32_t m = word_owner ? hs[tid] : 0u, nb0 = tid + 1 < (int)kWords ? hs[tid + 1] & 1u : 0u;
                     for (uint32_t cand = m & ~((m >> 1) | (nb0 << 31)); cand; cand &= cand - 1u) {
                         const uint32_t st = 32u * (uint32_t)tid + (uint32_t)__builtin_ctz(cand);
                         uint32_t en = nk;   // the next run start (bits past nk are 0)
@@ -1180,7 +1187,9 @@ __global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(2)
             // ------------------------------------------------ run-length encoding
             // (LDS-only barriers from here on: the next chunk's key loads stay in flight)
             uint32_t nu;
-            wpre[tid] = block_excl_scan<kCWaves, true>((uint32_t)__builtin_popcount(hh[tid]), wsum, &nu);
+            const uint32_t wx = block_excl_scan<kCWaves, true>(word_owner ? (uint32_t)__builtin_popcount(hh[tid]) : 0u,
+                                                               wsum, &nu);
+            if (word_owner) wpre[tid] = wx;
             tick(3);
             if (tid == 0) {
                 const uint32_t bf = lookback(cstatus, 1, flags, c, c0, nu, 1u);
