@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default="/dev/shm/kf_e2e" if os.access("/dev/shm", os.W_OK) else "/tmp/kf_e2e")
     ap.add_argument("--modes", default="read", help="variants to A/B in one process: name[:ENV=VAL[+ENV=VAL]],... "
-                    "(name read/register also sets KF_READ_MODE)")
+                    "(e.g. read,r1:KF_READERS=1)")
     ap.add_argument("--k", type=int, default=7)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
@@ -86,8 +86,6 @@ def main():
     for spec in [m for m in args.modes.split(",") if m]:
         name, _, envs = spec.partition(":")
         env = dict(kv.split("=", 1) for kv in envs.split("+") if kv)
-        if name in ("read", "register"):
-            env.setdefault("KF_READ_MODE", name)
         variants[name] = env
     modes = list(variants)
     base_env = {k: os.environ.get(k) for e in variants.values() for k in e}
