@@ -168,7 +168,8 @@ int kf_count_launch_info(int k, int* grid, int* block, int* lds_bytes);
  * goff[g] distinct k-mers, so both arrays hold batch_bytes = goff[n] entries).
  * The device counts each genome's keys per bucket (their top min(10, 2k)
  * bits), scatters every window's key once into its bucket (decoupled
- * look-back per bucket), packs whole buckets into chunks of <= 16,384 keys and
+ * look-back per bucket), packs whole buckets into chunks of <= 16,384 keys
+ * (12,288 for k <= 16) and
  * sorts each chunk in LDS (10-bit MSD passes plus a fix-up of runs of equal
  * top bits); buckets larger than a chunk are sorted by LSD passes in an
  * overflow area.  Then run-length encoding.  d_work must hold

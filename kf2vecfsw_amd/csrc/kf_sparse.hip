@@ -86,13 +86,14 @@ constexpr int kCBlock = KF_SP_CBLOCK;
 constexpr int kCWaves = kCBlock / 64;
 constexpr uint32_t kCCap = (uint32_t)KF_SP_CPER * (uint32_t)kCBlock;
 constexpr int kCPerCU = kCBlock >= 512 ? 1 : 512 / kCBlock;   // resident chunk workgroups per CU
-constexpr int kCWavesPerEU = (kCWaves * kCPerCU + 3) / 4;
-template <typename KeyT>
-struct ChunkOf {
-    static constexpr uint32_t cap = kCCap;                          // keys
-    static constexpr int per = cap / kCBlock;                       // keys per thread
-    static constexpr uint32_t wave_span = cap / kCWaves;
-};
+// u32 keys (k <= 16): 24 keys per thread, 12,288-key chunks, so a chunk
+// workgroup needs <= 80 KiB of LDS and two share a CU (4 waves per SIMD; the
+// 128-VGPR budget spills ~140 B per lane): k = 13 5.67-5.68 ms against
+// 5.84 with one 16,384-key workgroup per CU, k = 16 5.86-5.87 against 5.95
+// (processes alternated, profiles/r06/v33_sparse_u32_2wg_ab.jsonl)
+#ifndef KF_SP_CPER4
+#define KF_SP_CPER4 24
+#endif
 constexpr uint32_t kNoOvf = 0xFFFFFFFFu;
 // 8-bit MSD passes over the top bits of a chunk's keys before the run fix-up
 // (tools/ A/B builds: KF_SP_MSD=3 sorts 24 bits, leaving almost no runs).
@@ -125,6 +126,17 @@ constexpr uint32_t kNoOvf = 0xFFFFFFFFu;
 constexpr int kDB = KF_SP_DIGIT;
 constexpr uint32_t kND = 1u << kDB;          // digits
 constexpr uint32_t kNWW = kND / 2;           // packed u16 counter words per wave
+template <typename KeyT>
+struct ChunkOf {
+    static constexpr int per = sizeof(KeyT) == 4 ? KF_SP_CPER4 : KF_SP_CPER;   // keys per thread
+    static constexpr uint32_t cap = (uint32_t)per * (uint32_t)kCBlock;         // keys
+    static constexpr uint32_t wave_span = cap / kCWaves;
+    // LDS: the key stage, the digit counters, the head-mask prefixes, wsum, cid
+    static constexpr uint32_t lds = cap * (uint32_t)sizeof(KeyT) + kCWaves * kNWW * 4 + (cap / 32) * 4 +
+                                    kCWaves * 4 + 16;
+    static constexpr int per_cu = kCPerCU == 1 && 2 * lds <= 160u * 1024u ? 2 : kCPerCU;
+    static constexpr int waves_per_eu = (kCWaves * per_cu + 3) / 4;
+};
 struct Chunk {          // one LDS sort unit: buckets [blo, blo + nb) of one genome
     uint32_t start;     // first slot in the bucketed keys
     uint32_t nkeys;
@@ -959,7 +971,7 @@ __device__ __forceinline__ uint32_t ceil_log2(uint32_t x) { return x <= 1 ? 0u :
 // soon as a chunk is sorted and first used when its sort starts, so their
 // latency hides behind the encoding.
 template <typename KeyT>
-__global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kCWavesPerEU))) sp2_chunk_kernel(const KeyT* __restrict__ kb, const KeyT* __restrict__ ovf,
+__global__ void __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(ChunkOf<KeyT>::waves_per_eu))) sp2_chunk_kernel(const KeyT* __restrict__ kb, const KeyT* __restrict__ ovf,
                                                             const Chunk* chunks, const uint32_t* cfirst, int n,
                                                             int bshift, const uint64_t* goff, uint32_t* flags,
                                                             uint64_t* cstatus, uint32_t* ticket,
@@ -1319,7 +1331,7 @@ uint64_t al256(uint64_t x) { return (x + 255) & ~255ull; }
 SpLayout sp_layout(int k, uint64_t batch_bytes, int32_t n) {
     SpLayout L;
     const uint64_t ks = k <= 16 ? 4 : 8;
-    const uint64_t cap = kCCap;   // ChunkOf<KeyT>::cap
+    const uint64_t cap = ks == 4 ? ChunkOf<uint32_t>::cap : ChunkOf<uint64_t>::cap;
     L.tiles = (uint32_t)(batch_bytes / kTB + (uint64_t)n + 1);
     // greedy packing: two consecutive chunks hold more than cap keys together
     L.cmax = (uint32_t)(2 * batch_bytes / cap + (uint64_t)n + 1);
@@ -1494,7 +1506,8 @@ int sp_run(const uint8_t* d_bytes, const uint64_t* d_goff, int32_t n, uint64_t b
         corder = at32(L.corder);
         hipLaunchKernelGGL(sp_order_kernel, dim3(L.cmax / kSBlock + 1), dim3(kSBlock), 0, s, at32(L.cfirst), n, corder);
     }
-    hipLaunchKernelGGL(sp2_chunk_kernel<KeyT>, dim3((uint32_t)(cus * kCPerCU)), dim3(kCBlock), ChunkOf<KeyT>::cap * sizeof(KeyT), s,
+    hipLaunchKernelGGL(sp2_chunk_kernel<KeyT>, dim3((uint32_t)(cus * ChunkOf<KeyT>::per_cu)), dim3(kCBlock),
+                       ChunkOf<KeyT>::cap * sizeof(KeyT), s,
                        kb, ovf, (const Chunk*)(work + L.chunks), at32(L.cfirst), n, B, d_goff, &tfirst[n + 1],
                        (uint64_t*)(work + L.cstatus), at32(L.cticket), corder, d_keys, d_counts,
                        (uint64_t*)(work + L.unq), prof);

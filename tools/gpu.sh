@@ -88,7 +88,7 @@ for step in "$@"; do
       for rep in 1 2; do
         for v in product ${step#sparsealt=}; do
           lib=""; [ "$v" = product ] || lib=kf2vecfsw_amd/libkf2vec_gpu_$v.so
-          run 200 "$OUT/sp_p.json" env ${lib:+KF2VEC_GPU_LIB=$REPO/$lib} python3 -u tools/sparse_bench.py --genomes 64 --k 13,31 --reps 5
+          run 200 "$OUT/sp_p.json" env ${lib:+KF2VEC_GPU_LIB=$REPO/$lib} python3 -u tools/sparse_bench.py --genomes 64 --k 13,16,31 --reps 5
           python3 -c "import json,sys;d=json.loads(open('$OUT/sp_p.json').read().strip().splitlines()[-1]);print(json.dumps({'lib':sys.argv[1],'ms':{k:v['ms'] for k,v in d['k'].items()},'ok':[v['totals_ok'] for v in d['k'].values()]}))" "$v" >> "$OUT/sparsealt_$n.jsonl"
         done
       done ;;
